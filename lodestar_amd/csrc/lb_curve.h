@@ -1,0 +1,199 @@
+// Short-Weierstrass (a = 0) group law in Jacobian coordinates, generic over the base
+// field (fp for G1: y^2 = x^3 + 4, fp2 for G2: y^2 = x^3 + 4(1+u)).
+// Replaces blst's POINTonE1/POINTonE2 arithmetic used by bls.PublicKey.aggregate
+// (packages/beacon-node/src/chain/bls/utils.ts:11) and by Pairing.mul_n_aggregate
+// (maybeBatch.ts:18-25).  Additions are complete with respect to the cases aggregation
+// meets (duplicate keys P == Q, and P == -Q), as SURVEY.md §8 a3 requires.
+#pragma once
+#include "lb_field.h"
+
+template <class F>
+struct jac {
+  F x, y, z;  // z == 0 <=> infinity
+};
+template <class F>
+struct aff {
+  F x, y;
+};
+
+typedef jac<fp> g1j;
+typedef jac<fp2> g2j;
+typedef aff<fp> g1a;
+typedef aff<fp2> g2a;
+
+template <class F>
+LB_HD jac<F> jac_infinity() {
+  jac<F> r;
+  f_set_one(r.x);
+  f_set_one(r.y);
+  f_set_zero(r.z);
+  return r;
+}
+template <class F>
+LB_HD bool jac_is_inf(const jac<F>& p) {
+  return f_is_zero(p.z);
+}
+template <class F>
+LB_HD jac<F> jac_from_aff(const aff<F>& a) {
+  jac<F> r;
+  r.x = a.x;
+  r.y = a.y;
+  f_set_one(r.z);
+  return r;
+}
+template <class F>
+LB_HD jac<F> jac_neg(const jac<F>& p) {
+  return jac<F>{p.x, f_neg(p.y), p.z};
+}
+
+// dbl-2009-l
+template <class F>
+LB_HD jac<F> jac_dbl(const jac<F>& p) {
+  F A = f_sqr(p.x);
+  F B = f_sqr(p.y);
+  F C = f_sqr(B);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
+  F E = f_mul3(A);
+  F Fv = f_sqr(E);
+  jac<F> r;
+  r.x = f_sub(Fv, f_dbl(D));
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), f_mul8(C));
+  r.z = f_dbl(f_mul(p.y, p.z));
+  return r;
+}
+
+// add-2007-bl with the exceptional cases handled
+template <class F>
+LB_HD jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, U1);
+  F rr = f_dbl(f_sub(S2, S1));
+  if (f_is_zero(H)) {
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F V = f_mul(U1, I);
+  jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
+  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return r;
+}
+
+// madd-2007-bl: p Jacobian + q affine (q not infinity)
+template <class F>
+LB_HD jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+  if (jac_is_inf(p)) return jac_from_aff(q);
+  F Z1Z1 = f_sqr(p.z);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, p.x);
+  F rr = f_dbl(f_sub(S2, p.y));
+  if (f_is_zero(H)) {
+    if (f_is_zero(rr)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F HH = f_sqr(H);
+  F I = f_dbl(f_dbl(HH));
+  F J = f_mul(H, I);
+  F V = f_mul(p.x, I);
+  jac<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
+  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  return r;
+}
+
+template <class F>
+LB_HD bool jac_eq(const jac<F>& p, const jac<F>& q) {
+  bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F Z1Z1 = f_sqr(p.z), Z2Z2 = f_sqr(q.z);
+  if (!f_eq(f_mul(p.x, Z2Z2), f_mul(q.x, Z1Z1))) return false;
+  return f_eq(f_mul(f_mul(p.y, q.z), Z2Z2), f_mul(f_mul(q.y, p.z), Z1Z1));
+}
+
+// to affine; returns false for infinity
+template <class F>
+LB_HD bool jac_to_aff(aff<F>& out, const jac<F>& p) {
+  F zi = f_inv(p.z);
+  F zi2 = f_sqr(zi);
+  out.x = f_mul(p.x, zi2);
+  out.y = f_mul(f_mul(p.y, zi2), zi);
+  return !jac_is_inf(p);
+}
+
+// [k]P for a 64-bit scalar, P affine (left-to-right double-and-add)
+template <class F>
+LB_HD jac<F> jac_mul_u64(const aff<F>& p, uint64_t k) {
+  jac<F> acc = jac_infinity<F>();
+  for (int i = 63; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((k >> i) & 1ull) acc = jac_add_aff(acc, p);
+  }
+  return acc;
+}
+
+// [|x|]P for the curve parameter |x| = 0xd201000000010000 (wave-uniform bits)
+template <class F>
+LB_HD jac<F> jac_mul_xabs(const jac<F>& p) {
+  jac<F> acc = p;  // top bit
+  for (int i = 62; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((LB_X_ABS >> i) & 1ull) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+// ------------------------------------------------------------------ G2 endomorphism psi
+LB_HD g2j g2_psi(const g2j& p) {
+  g2j r;
+  r.x = fp2_mul(fp2_conj(p.x), fp2_load(LB_PSI_CX));
+  r.y = fp2_mul(fp2_conj(p.y), fp2_load(LB_PSI_CY));
+  r.z = fp2_conj(p.z);
+  return r;
+}
+LB_HD g2j g2_psi2(const g2j& p) {
+  g2j r;
+  r.x = fp2_mul_fp(p.x, fp_load(LB_PSI2_CX));
+  r.y = fp2_mul_fp(p.y, fp_load(LB_PSI2_CY));
+  r.z = p.z;
+  return r;
+}
+
+// Scott's G2 membership test (the one blst uses): P in G2 <=> psi(P) == [x]P, x < 0.
+LB_HD bool g2_in_subgroup(const g2j& p) {
+  if (jac_is_inf(p)) return true;
+  g2j xp = jac_neg(jac_mul_xabs(p));
+  return jac_eq(g2_psi(p), xp);
+}
+
+// h_eff * P via psi (RFC 9380 App. G.3 / Budroni-Pintore)
+LB_HD g2j g2_clear_cofactor(const g2j& p) {
+  g2j t1 = jac_neg(jac_mul_xabs(p));  // [x]P
+  g2j t2 = g2_psi(p);
+  g2j t3 = g2_psi2(jac_dbl(p));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = jac_neg(jac_mul_xabs(t2));  // [x](t1 + t2)
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(p));
+}
+
+// G1 curve check (affine, y^2 == x^3 + 4)
+LB_HD bool g1_aff_on_curve(const g1a& a) {
+  return fp_eq(fp_sqr(a.y), fp_add(fp_mul(fp_sqr(a.x), a.x), fp_load(LB_B1)));
+}
+LB_HD bool g2_aff_on_curve(const g2a& a) {
+  return fp2_eq(fp2_sqr(a.y), fp2_add(fp2_mul(fp2_sqr(a.x), a.x), fp2_load(LB_B2)));
+}

@@ -1,0 +1,414 @@
+// BLS12-381 field tower for gfx950: Fp (12 x u32 Montgomery limbs), Fp2 = Fp[u]/(u^2+1),
+// Fp6 = Fp2[v]/(v^3 - (1+u)), Fp12 = Fp6[w]/(w^2 - v).
+//
+// Replaces the blst field layer that @chainsafe/blst@0.2.7 runs under
+// packages/beacon-node/src/chain/bls/maybeBatch.ts:18-37.
+// Every element is kept fully reduced in [0, p) in Montgomery form (R = 2^384), so
+// equality is limb equality and serialisation is one Montgomery multiply away.
+// The 32x32->64 multiply-accumulate chains lower to v_mad_u64_u32 on gfx950.
+#pragma once
+#include "lb_common.h"
+#include "lb_consts.h"
+
+struct fp {
+  uint32_t v[12];
+};
+struct fp2 {
+  fp c0, c1;
+};
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ------------------------------------------------------------------ Fp basics
+LB_HD fp fp_load(const uint32_t* c) {
+  fp r;
+  LB_UNROLL for (int i = 0; i < 12; i++) r.v[i] = c[i];
+  return r;
+}
+LB_HD fp2 fp2_load(const uint32_t* c) {
+  fp2 r;
+  r.c0 = fp_load(c);
+  r.c1 = fp_load(c + 12);
+  return r;
+}
+LB_HD fp fp_zero() {
+  fp r;
+  LB_UNROLL for (int i = 0; i < 12; i++) r.v[i] = 0;
+  return r;
+}
+LB_HD fp fp_one() { return fp_load(LB_ONE); }
+
+LB_HD bool fp_is_zero(const fp& a) {
+  uint32_t t = 0;
+  LB_UNROLL for (int i = 0; i < 12; i++) t |= a.v[i];
+  return t == 0;
+}
+LB_HD bool fp_eq(const fp& a, const fp& b) {
+  uint32_t t = 0;
+  LB_UNROLL for (int i = 0; i < 12; i++) t |= a.v[i] ^ b.v[i];
+  return t == 0;
+}
+LB_HD fp fp_select(bool c, const fp& a, const fp& b) {
+  fp r;
+  LB_UNROLL for (int i = 0; i < 12; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// r = a - p if a >= p (a given as 12 limbs + carry word)
+LB_HD fp fp_reduce_once(const uint32_t* t, uint32_t top) {
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t s[12];
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    uint64_t d = (uint64_t)t[j] - Pl[j] - br;
+    s[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  bool ge = (top != 0) || (br == 0);
+  fp r;
+  LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = ge ? s[j] : t[j];
+  return r;
+}
+
+LB_HD fp fp_add(const fp& a, const fp& b) {
+  uint32_t t[12];
+  uint64_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    c = (uint64_t)a.v[j] + b.v[j] + (c >> 32);
+    t[j] = (uint32_t)c;
+  }
+  return fp_reduce_once(t, (uint32_t)(c >> 32));
+}
+
+LB_HD fp fp_sub(const fp& a, const fp& b) {
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t t[12];
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    uint64_t d = (uint64_t)a.v[j] - b.v[j] - br;
+    t[j] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  // if borrow, add p back
+  uint32_t m = 0u - br;
+  fp r;
+  uint64_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    c = (uint64_t)t[j] + (Pl[j] & m) + (c >> 32);
+    r.v[j] = (uint32_t)c;
+  }
+  return r;
+}
+
+LB_HD fp fp_neg(const fp& a) { return fp_sub(fp_zero(), a); }
+LB_HD fp fp_dbl(const fp& a) { return fp_add(a, a); }
+
+// Montgomery multiplication, CIOS with 32-bit limbs: a*b/R mod p.
+LB_HD fp fp_mul(const fp& a, const fp& b) {
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t t[14];
+  LB_UNROLL for (int j = 0; j < 14; j++) t[j] = 0;
+  LB_UNROLL for (int i = 0; i < 12; i++) {
+    uint64_t c = 0;
+    LB_UNROLL for (int j = 0; j < 12; j++) {
+      c = (uint64_t)a.v[i] * b.v[j] + t[j] + (c >> 32);
+      t[j] = (uint32_t)c;
+    }
+    c = (uint64_t)t[12] + (c >> 32);
+    t[12] = (uint32_t)c;
+    t[13] = (uint32_t)(c >> 32);
+    uint32_t m = t[0] * LB_PINV;
+    c = (uint64_t)m * Pl[0] + t[0];
+    LB_UNROLL for (int j = 1; j < 12; j++) {
+      c = (uint64_t)m * Pl[j] + t[j] + (c >> 32);
+      t[j - 1] = (uint32_t)c;
+    }
+    c = (uint64_t)t[12] + (c >> 32);
+    t[11] = (uint32_t)c;
+    t[12] = t[13] + (uint32_t)(c >> 32);
+  }
+  return fp_reduce_once(t, t[12]);
+}
+
+LB_HD fp fp_sqr(const fp& a) { return fp_mul(a, a); }
+
+// small-constant multiples via additions
+LB_HD fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
+LB_HD fp fp_mul4(const fp& a) { return fp_dbl(fp_dbl(a)); }
+LB_HD fp fp_mul8(const fp& a) { return fp_dbl(fp_mul4(a)); }
+
+LB_HD fp fp_to_mont(const fp& a) { return fp_mul(a, fp_load(LB_R2)); }
+LB_HD fp fp_from_mont(const fp& a) {
+  fp one = fp_zero();
+  one.v[0] = 1;
+  return fp_mul(a, one);
+}
+
+// a^e for a compile-time-constant exponent held in (constant) memory; the exponent
+// bits are wave-uniform so the branch is a scalar branch on the GPU.
+LB_HD fp fp_pow_const(const fp& a, const uint32_t* e, int top_bit) {
+  fp r = a;
+  for (int i = top_bit - 1; i >= 0; i--) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+LB_HD fp fp_inv(const fp& a) { return fp_pow_const(a, LB_EXP_PM2, 380); }          // a^(p-2); inv(0)=0
+LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
+LB_HD bool fp_is_square(const fp& a) {
+  // Legendre symbol a^((p-1)/2) in {0, 1, -1}
+  fp l = fp_pow_const(a, LB_EXP_LEGENDRE, 379);
+  return fp_is_zero(a) || fp_eq(l, fp_one());
+}
+
+// canonical (non-Montgomery) value compared with (p-1)/2: returns a > (p-1)/2
+LB_HD bool fp_plain_gt_half(const fp& plain) {
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    uint64_t d = (uint64_t)LB_HALF_P[j] - plain.v[j] - br;
+    br = (uint32_t)(d >> 63);
+  }
+  return br != 0;  // half - a < 0
+}
+
+// 48-byte big-endian -> plain limbs; returns false if value >= p (blst BAD_ENCODING)
+LB_HD bool fp_plain_from_be48(fp& out, const uint8_t* b, uint8_t first_byte_mask) {
+  LB_UNROLL for (int i = 0; i < 12; i++) {
+    int o = 44 - 4 * i;
+    uint32_t b0 = b[o];
+    if (i == 11) b0 &= first_byte_mask;
+    out.v[i] = (b0 << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) | b[o + 3];
+  }
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    uint64_t d = (uint64_t)out.v[j] - Pl[j] - br;
+    br = (uint32_t)(d >> 63);
+  }
+  return br != 0;  // out < p
+}
+
+LB_HD void fp_plain_to_be48(uint8_t* b, const fp& plain) {
+  LB_UNROLL for (int i = 0; i < 12; i++) {
+    int o = 44 - 4 * i;
+    uint32_t w = plain.v[i];
+    b[o] = (uint8_t)(w >> 24);
+    b[o + 1] = (uint8_t)(w >> 16);
+    b[o + 2] = (uint8_t)(w >> 8);
+    b[o + 3] = (uint8_t)w;
+  }
+}
+
+// ------------------------------------------------------------------ Fp2
+LB_HD fp2 fp2_zero() { return fp2{fp_zero(), fp_zero()}; }
+LB_HD fp2 fp2_one() { return fp2{fp_one(), fp_zero()}; }
+LB_HD bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+LB_HD bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+LB_HD fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return fp2{fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+LB_HD fp2 fp2_add(const fp2& a, const fp2& b) { return fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+LB_HD fp2 fp2_sub(const fp2& a, const fp2& b) { return fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+LB_HD fp2 fp2_dbl(const fp2& a) { return fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+LB_HD fp2 fp2_neg(const fp2& a) { return fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
+LB_HD fp2 fp2_conj(const fp2& a) { return fp2{a.c0, fp_neg(a.c1)}; }
+LB_HD fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+LB_HD fp2 fp2_mul3(const fp2& a) { return fp2{fp_mul3(a.c0), fp_mul3(a.c1)}; }
+LB_HD fp2 fp2_mul4(const fp2& a) { return fp2{fp_mul4(a.c0), fp_mul4(a.c1)}; }
+LB_HD fp2 fp2_mul8(const fp2& a) { return fp2{fp_mul8(a.c0), fp_mul8(a.c1)}; }
+
+LB_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp t0 = fp_mul(a.c0, b.c0);
+  fp t1 = fp_mul(a.c1, b.c1);
+  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+LB_HD fp2 fp2_sqr(const fp2& a) {
+  fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp t1 = fp_mul(a.c0, a.c1);
+  return fp2{t0, fp_dbl(t1)};
+}
+// multiply by the non-residue xi = 1 + u
+LB_HD fp2 fp2_mul_xi(const fp2& a) { return fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+LB_HD fp2 fp2_inv(const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp ni = fp_inv(n);
+  return fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+LB_HD bool fp2_is_square(const fp2& a) { return fp_is_square(fp_add(fp_sqr(a.c0), fp_sqr(a.c1))); }
+
+// Square root in Fp2 by the complex method (p = 3 mod 4): three Fp exponentiations,
+// no data-dependent branches.  Returns true iff a is a square; `out` is some root.
+LB_HD bool fp2_sqrt(fp2& out, const fp2& a) {
+  fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
+  fp inv2 = fp_load(LB_INV2);
+  fp d1 = fp_mul(fp_add(a.c0, alpha), inv2);
+  fp d2 = fp_mul(fp_sub(a.c0, alpha), inv2);
+  // (a0 + alpha)/2 is zero only when a1 == 0 and alpha == -a0; use the other candidate
+  fp delta = fp_select(fp_is_zero(d1), d2, d1);
+  fp s = fp_sqrt_cand(delta);
+  bool delta_qr = fp_eq(fp_sqr(s), delta);
+  // if delta is a residue: x0 = s, x1 = a1/(2s); else x0 = a1/(2s), x1 = s
+  fp t = fp_inv(fp_dbl(s));
+  fp q = fp_mul(a.c1, t);
+  out.c0 = fp_select(delta_qr, s, q);
+  out.c1 = fp_select(delta_qr, q, s);
+  return fp2_eq(fp2_sqr(out), a);
+}
+
+// RFC 9380 sgn0 for Fp2 (on canonical values)
+LB_HD uint32_t fp2_sgn0(const fp2& a) {
+  fp p0 = fp_from_mont(a.c0), p1 = fp_from_mont(a.c1);
+  uint32_t sign0 = p0.v[0] & 1u;
+  uint32_t zero0 = fp_is_zero(p0) ? 1u : 0u;
+  uint32_t sign1 = p1.v[0] & 1u;
+  return sign0 | (zero0 & sign1);
+}
+
+// ZCash "lexicographically largest" for Fp2: decided by c1 unless c1 == 0
+LB_HD bool fp2_lex_larger(const fp2& a) {
+  fp p0 = fp_from_mont(a.c0), p1 = fp_from_mont(a.c1);
+  return fp_is_zero(p1) ? fp_plain_gt_half(p0) : fp_plain_gt_half(p1);
+}
+
+// ------------------------------------------------------------------ Fp6
+LB_HD fp6 fp6_zero() { return fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
+LB_HD fp6 fp6_one() { return fp6{fp2_one(), fp2_zero(), fp2_zero()}; }
+LB_HD fp6 fp6_add(const fp6& a, const fp6& b) { return fp6{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+LB_HD fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+LB_HD fp6 fp6_neg(const fp6& a) { return fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+LB_HD fp6 fp6_mul_v(const fp6& a) { return fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+LB_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
+  fp2 t0 = fp2_mul(a.c0, b.c0);
+  fp2 t1 = fp2_mul(a.c1, b.c1);
+  fp2 t2 = fp2_mul(a.c2, b.c2);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
+  fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  return fp6{c0, c1, c2};
+}
+
+// a * (b0 + b1 v)  (sparse: c2 coefficient zero)
+LB_HD fp6 fp6_mul_01(const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 t0 = fp2_mul(a.c0, b0);
+  fp2 t1 = fp2_mul(a.c1, b1);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), t0);
+  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  fp2 c2 = fp2_add(fp2_mul(a.c2, b0), t1);
+  return fp6{c0, c1, c2};
+}
+
+// a * (b1 v)
+LB_HD fp6 fp6_mul_1(const fp6& a, const fp2& b1) {
+  return fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+LB_HD fp6 fp6_inv(const fp6& a) {
+  fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  fp2 d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  fp2 di = fp2_inv(d);
+  return fp6{fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ------------------------------------------------------------------ Fp12
+LB_HD fp12 fp12_one() { return fp12{fp6_one(), fp6_zero()}; }
+LB_HD bool fp12_is_one(const fp12& a) {
+  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) &&
+         fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
+}
+LB_HD fp12 fp12_conj(const fp12& a) { return fp12{a.c0, fp6_neg(a.c1)}; }
+
+LB_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
+  fp6 t0 = fp6_mul(a.c0, b.c0);
+  fp6 t1 = fp6_mul(a.c1, b.c1);
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return fp12{c0, c1};
+}
+
+LB_HD fp12 fp12_sqr(const fp12& a) {
+  // complex squaring: (a0 + a1 w)^2 = a0^2 + v a1^2 + 2 a0 a1 w
+  fp6 t = fp6_mul(a.c0, a.c1);
+  fp6 c0 = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  c0 = fp6_sub(fp6_sub(c0, t), fp6_mul_v(t));
+  return fp12{c0, fp6_add(t, t)};
+}
+
+// multiply by a Miller-loop line  l = (l0 + l2 v) + (l3 v) w   (w-basis: l0 w^0 + l2 w^2 + l3 w^3)
+LB_HD fp12 fp12_mul_line(const fp12& a, const fp2& l0, const fp2& l2, const fp2& l3) {
+  fp6 t0 = fp6_mul_01(a.c0, l0, l2);
+  fp6 t1 = fp6_mul_1(a.c1, l3);
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(a.c0, a.c1), l0, fp2_add(l2, l3)), t0), t1);
+  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return fp12{c0, c1};
+}
+
+LB_HD fp12 fp12_inv(const fp12& a) {
+  fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
+  fp6 ti = fp6_inv(t);
+  return fp12{fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti))};
+}
+
+// Frobenius a -> a^p.  In the w-basis a = sum a_k w^k (a_0=c0.c0, a_1=c1.c0, a_2=c0.c1,
+// a_3=c1.c1, a_4=c0.c2, a_5=c1.c2), a^p = sum conj(a_k) xi^(k(p-1)/6) w^k.
+LB_HD fp12 fp12_frob(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), fp2_load(LB_FROB1_1));
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), fp2_load(LB_FROB1_2));
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), fp2_load(LB_FROB1_3));
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), fp2_load(LB_FROB1_4));
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), fp2_load(LB_FROB1_5));
+  return r;
+}
+LB_HD fp12 fp12_frob2(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fp2_mul_fp(a.c1.c0, fp_load(LB_FROB2_1));
+  r.c0.c1 = fp2_mul_fp(a.c0.c1, fp_load(LB_FROB2_2));
+  r.c1.c1 = fp2_mul_fp(a.c1.c1, fp_load(LB_FROB2_3));
+  r.c0.c2 = fp2_mul_fp(a.c0.c2, fp_load(LB_FROB2_4));
+  r.c1.c2 = fp2_mul_fp(a.c1.c2, fp_load(LB_FROB2_5));
+  return r;
+}
+
+// ------------------------------------------------------------------ overloads for generic curve code
+LB_HD fp f_add(const fp& a, const fp& b) { return fp_add(a, b); }
+LB_HD fp f_sub(const fp& a, const fp& b) { return fp_sub(a, b); }
+LB_HD fp f_mul(const fp& a, const fp& b) { return fp_mul(a, b); }
+LB_HD fp f_sqr(const fp& a) { return fp_sqr(a); }
+LB_HD fp f_dbl(const fp& a) { return fp_dbl(a); }
+LB_HD fp f_neg(const fp& a) { return fp_neg(a); }
+LB_HD fp f_mul3(const fp& a) { return fp_mul3(a); }
+LB_HD fp f_mul8(const fp& a) { return fp_mul8(a); }
+LB_HD fp f_inv(const fp& a) { return fp_inv(a); }
+LB_HD bool f_is_zero(const fp& a) { return fp_is_zero(a); }
+LB_HD bool f_eq(const fp& a, const fp& b) { return fp_eq(a, b); }
+LB_HD fp f_select(bool c, const fp& a, const fp& b) { return fp_select(c, a, b); }
+LB_HD void f_set_zero(fp& a) { a = fp_zero(); }
+LB_HD void f_set_one(fp& a) { a = fp_one(); }
+
+LB_HD fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
+LB_HD fp2 f_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
+LB_HD fp2 f_mul(const fp2& a, const fp2& b) { return fp2_mul(a, b); }
+LB_HD fp2 f_sqr(const fp2& a) { return fp2_sqr(a); }
+LB_HD fp2 f_dbl(const fp2& a) { return fp2_dbl(a); }
+LB_HD fp2 f_neg(const fp2& a) { return fp2_neg(a); }
+LB_HD fp2 f_mul3(const fp2& a) { return fp2_mul3(a); }
+LB_HD fp2 f_mul8(const fp2& a) { return fp2_mul8(a); }
+LB_HD fp2 f_inv(const fp2& a) { return fp2_inv(a); }
+LB_HD bool f_is_zero(const fp2& a) { return fp2_is_zero(a); }
+LB_HD bool f_eq(const fp2& a, const fp2& b) { return fp2_eq(a, b); }
+LB_HD fp2 f_select(bool c, const fp2& a, const fp2& b) { return fp2_select(c, a, b); }
+LB_HD void f_set_zero(fp2& a) { a = fp2_zero(); }
+LB_HD void f_set_one(fp2& a) { a = fp2_one(); }

@@ -1,0 +1,105 @@
+// Optimal-ate Miller loop and final exponentiation for BLS12-381 (M-type sextic twist,
+// y^2 = x^3 + 4(1+u)).  Replaces blst's miller_loop_n / final_exp behind
+// Pairing.commit + Pairing.finalverify (maybeBatch.ts:18-25).
+//
+// Lines are evaluated at the G1 point P = (xP, yP) and kept in the sparse form
+//   l = l0 + l2 w^2 + l3 w^3      (Fp12 = Fp6[w]/(w^2 - v))
+// which differs from the textbook line value only by factors in Fp4, killed by the
+// final exponentiation.  The hard part computes f^(3(p^4-p^2+1)/r); cubing is a
+// bijection on the order-r group, so "== 1" decides exactly as blst's finalverify.
+#pragma once
+#include "lb_curve.h"
+
+// doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P
+LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+  const fp2 b3 = fp2_load(LB_B2_3);  // 3 b'
+  fp2 X = T.x, Y = T.y, Z = T.z;
+  fp2 A = fp2_mul(X, Y);             // XY (halved below)
+  fp2 B = fp2_sqr(Y);
+  fp2 C = fp2_sqr(Z);
+  fp2 E = fp2_mul(b3, C);            // 3b' Z^2
+  fp2 F = fp2_mul3(E);               // 9b' Z^2
+  fp2 G = fp2_add(B, F);             // (B + F), halved below
+  fp2 H = fp2_sub(fp2_sqr(fp2_add(Y, Z)), fp2_add(B, C));  // 2YZ
+  fp2 XX3 = fp2_mul3(fp2_sqr(X));
+  // line: (B - E) + (-3X^2 xP) w^2 + (H yP) w^3
+  l0 = fp2_sub(B, E);
+  l2 = fp2_neg(fp2_mul_fp(XX3, xP));
+  l3 = fp2_mul_fp(H, yP);
+  // X3 = XY/2 (B - F);  Y3 = ((B+F)/2)^2 - 3E^2;  Z3 = B H
+  fp inv2 = fp_load(LB_INV2);
+  fp2 A2 = fp2_mul_fp(A, inv2);
+  fp2 G2 = fp2_mul_fp(G, inv2);
+  T.x = fp2_mul(A2, fp2_sub(B, F));
+  T.y = fp2_sub(fp2_sqr(G2), fp2_mul3(fp2_sqr(E)));
+  T.z = fp2_mul(B, H);
+}
+
+// addition step T <- T + Q (Q affine), line through T and Q at P
+LB_HD void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+  fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
+  fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  // line: (theta xQ - lam yQ) + (-theta xP) w^2 + (lam yP) w^3
+  l0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
+  l2 = fp2_neg(fp2_mul_fp(theta, xP));
+  l3 = fp2_mul_fp(lam, yP);
+  fp2 C = fp2_sqr(theta);
+  fp2 D = fp2_sqr(lam);
+  fp2 E = fp2_mul(lam, D);
+  fp2 F = fp2_mul(T.z, C);
+  fp2 G = fp2_mul(T.x, D);
+  fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
+  T.x = fp2_mul(lam, H);
+  T.y = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), fp2_mul(E, T.y));
+  T.z = fp2_mul(T.z, E);
+}
+
+// f_{|x|,Q}(P), conjugated (x < 0).  P, Q affine and not infinity.
+LB_HD fp12 miller_loop(const g1a& P, const g2a& Q) {
+  g2j T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  fp2 l0, l2, l3;
+  fp12 f = fp12_one();
+  bool first = true;
+  for (int i = 62; i >= 0; i--) {
+    if (!first) f = fp12_sqr(f);
+    miller_dbl(T, l0, l2, l3, P.x, P.y);
+    if (first) {
+      f = fp12_one();
+      first = false;
+    }
+    f = fp12_mul_line(f, l0, l2, l3);
+    if ((LB_X_ABS >> i) & 1ull) {
+      miller_add(T, Q, l0, l2, l3, P.x, P.y);
+      f = fp12_mul_line(f, l0, l2, l3);
+    }
+  }
+  return fp12_conj(f);
+}
+
+// a^|x| for a in the cyclotomic subgroup
+LB_HD fp12 fp12_pow_xabs(const fp12& a) {
+  fp12 r = a;
+  for (int i = 62; i >= 0; i--) {
+    r = fp12_sqr(r);
+    if ((LB_X_ABS >> i) & 1ull) r = fp12_mul(r, a);
+  }
+  return r;
+}
+
+// f^(3 (p^12 - 1)/r)
+LB_HD fp12 final_exponentiation(const fp12& f) {
+  // easy part: f^((p^6 - 1)(p^2 + 1))
+  fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));
+  t = fp12_mul(fp12_frob2(t), t);
+  // hard part: t^((x-1)^2 (x+p) (x^2+p^2-1) + 3)
+  fp12 a = fp12_conj(fp12_mul(fp12_pow_xabs(t), t));  // t^(x-1)
+  a = fp12_conj(fp12_mul(fp12_pow_xabs(a), a));        // t^((x-1)^2)
+  fp12 b = fp12_mul(fp12_conj(fp12_pow_xabs(a)), fp12_frob(a));  // a^(x+p)
+  fp12 c = fp12_pow_xabs(fp12_pow_xabs(b));                        // b^(x^2)
+  c = fp12_mul(fp12_mul(c, fp12_frob2(b)), fp12_conj(b));          // b^(x^2+p^2-1)
+  fp12 t3 = fp12_mul(fp12_sqr(t), t);
+  return fp12_mul(c, t3);
+}
