@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Benchmark: verified signature sets/s on the mainnet gossip attestation mix (BASELINE.json
+metric; workload c3 = configs[2], one slot's gossip flood: 16384 attestation sets + 1024
+aggregate-and-proof calls x 3 sets, 17408 jobs / 19456 sets per GPU).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3] [--no-cpu-baseline]
+
+One process per GPU (torchrun for N>1; RANK/LOCAL_RANK/WORLD_SIZE from the env).  Each rank
+verifies its own slot-sized shard (weak scaling: sets shard across GPUs with no data-path
+collective; the optional --exchange flag adds the 576-byte Fp12 partial all-gather over RCCL
+and one final exponentiation).  A step = lb_batch_verify over the resident
+batch: all kernels + CSPRNG scalars + per-job result readback.  Inputs are in HBM before the
+timed region.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--exchange", action="store_true", help="RCCL all-gather of Fp12 partials per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    return ap.parse_args()
+
+
+def load_counts():
+    p = os.path.join(ROOT, "profiles", "roofline_counts.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+
+    eng = Engine(local)
+    t0 = time.time()
+    wl = W.make(eng, a.workload, seed=W.SEED + rank)
+    gen_s = time.time() - t0
+    batch = eng.upload(wl.packed)
+    n_sets, n_jobs = wl.packed.n_sets, wl.packed.n_jobs
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def step():
+        if a.exchange and world > 1:
+            f, st = batch.partial()
+            t = torch.frombuffer(bytearray(f), dtype=torch.uint8).cuda()
+            g = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(g, t)
+            ok = eng.product_is_one([x.cpu().numpy().tobytes() for x in g])
+            codes = st if ok else batch.verify()
+        else:
+            codes = batch.verify()
+        return codes
+
+    for _ in range(a.warmup):
+        codes = step()
+    assert np.array_equal(np.asarray(codes) == 1, wl.expected == 1), "verification results differ from expected"
+
+    eng.set_profiling(True)
+    stage_ms = {}
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        codes = step()
+        for k, v in eng.last_profile().items():
+            stage_ms[k] = stage_ms.get(k, 0.0) + v
+    barrier()
+    el = time.perf_counter() - t1
+    eng.set_profiling(False)
+    el_t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    ms_per_step = el / a.steps * 1e3
+    value = n_sets * world * a.steps / el
+    stage_ms = {k: v / a.steps for k, v in stage_ms.items()}
+
+    roof = None
+    counts = load_counts()
+    if counts:
+        dom = max((k for k in stage_ms if k in counts["per_launch_mul"]), key=lambda k: stage_ms[k], default=None)
+        if dom:
+            muls = counts["per_launch_mul"][dom](n_sets) if callable(counts["per_launch_mul"][dom]) else None
+            per_item = counts["per_item_mul"][dom]
+            items = n_sets * counts["items_per_set"].get(dom, 1)
+            mul_total = per_item * items
+            ach = mul_total / (stage_ms[dom] * 1e-3) / 1e12
+            peak = counts["peak_tmul_s"]
+            roof = {"bound": "valu-int", "kernel": "k_" + dom, "achieved": round(ach, 4), "peak": peak,
+                    "unit": "T int32-mul/s", "frac": round(ach / peak, 4), "traffic": counts.get("traffic", {}).get(dom),
+                    "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            from oracle.cpu_pool import time_cpu_pool
+            cpu = time_cpu_pool(wl.packed, seconds=a.cpu_seconds, threads=a.cpu_threads)
+        except Exception as e:  # reported, never fatal
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps({
+            "metric": "verified signature sets/sec (mainnet attestation mix)",
+            "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)", "data": "synthetic",
+            "config": {"workload": f"{a.workload}: gossip attestation flood, one slot per GPU" if a.workload == "c3"
+                       else a.workload, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
+                       "pubkeys_per_gpu": int(wl.packed.pk_off[-1]), "parallelism": f"dp{world} (sets sharded)",
+                       "exchange": bool(a.exchange)},
+            "roofline": roof, "cpu_baseline": cpu, "gen_s": round(gen_s, 2),
+        }), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,152 @@
+/*
+ * lodestar_bls.h — C ABI of the MI355X BLS12-381 signature-set verifier.
+ *
+ * This is the drop-in boundary for Lodestar's IBlsVerifier hot path
+ * (SURVEY.md §8(b)).  Plain pointers and sizes only; no torch / HIP types.
+ * Every entry point returns an lb_status code (0 = OK) and never throws.
+ *
+ * Reference interfaces each entry point replaces (paths under the reference repo):
+ *   lb_verify_jobs / lb_batch_*   packages/beacon-node/src/chain/bls/multithread/worker.ts:32-108
+ *                                 (verifyManySignatureSets: BlsWorkReq[] -> per-job results),
+ *                                 packages/beacon-node/src/chain/bls/maybeBatch.ts:16-39
+ *                                 (verifySignatureSetsMaybeBatch) and the blst calls it makes
+ *                                 (Signature.fromBytes(sig, affine, true), verifyMultipleSignatures,
+ *                                 Signature.verify).
+ *   lb_aggregate_pubkeys          packages/beacon-node/src/chain/bls/utils.ts:5-16
+ *                                 (getAggregatedPubkey) + PublicKey.toBytes(uncompressed),
+ *                                 packages/beacon-node/src/chain/bls/multithread/index.ts:126,160.
+ *   lb_batch_partial /
+ *   lb_fp12_product_is_one        the multi-GPU split of blst Pairing.commit()+finalverify()
+ *                                 (SURVEY.md §8(e)): per-GPU Fp12 partial products, one
+ *                                 final exponentiation over their product.
+ *
+ * Data formats (all ZCash BLS12-381 encodings, big-endian):
+ *   pubkey      96 B uncompressed affine G1 (x || y), as the reference's main thread
+ *               serialises it (PointFormat.uncompressed); infinity = 0x40 || 0^95.
+ *   signing root 32 B (ISignatureSet.signingRoot).
+ *   signature   96 B compressed G2 (ISignatureSet.signature).
+ *   Fp12 partial 576 B: 12 Fp coefficients, tower order c0.c0.c0, c0.c0.c1, c0.c1.c0, ...
+ *
+ * Job results (int32 per job): 1 = valid, 0 = invalid, -code = the job rejects with
+ * error `code` (lb_error_name(code) gives the blst error string the reference throws).
+ */
+#ifndef LODESTAR_BLS_H
+#define LODESTAR_BLS_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status / error codes: blst BLST_ERROR values plus Lodestar's own errors */
+#define LB_OK 0
+#define LB_BAD_ENCODING 1
+#define LB_POINT_NOT_ON_CURVE 2
+#define LB_POINT_NOT_IN_GROUP 3
+#define LB_AGGR_TYPE_MISMATCH 4
+#define LB_VERIFY_FAIL 5
+#define LB_PK_IS_INFINITY 6
+#define LB_BAD_SCALAR 7
+#define LB_INVALID_SIZE 10           /* "BLST_INVALID_SIZE" (multithread.test.ts:97) */
+#define LB_EMPTY_AGGREGATE_ARRAY 11  /* bls.PublicKey.aggregate([]) */
+#define LB_EMPTY_SIGNATURE_SET 12    /* "Empty signature set" (maybeBatch.ts:29-31) */
+#define LB_ERR_ARGUMENT 100          /* bad C-ABI arguments (NULL, inconsistent offsets) */
+#define LB_ERR_DEVICE 101            /* HIP runtime failure */
+#define LB_ERR_NO_DEVICE 102         /* no usable gfx950 device */
+
+typedef struct lb_engine lb_engine;
+typedef struct lb_batch lb_batch;
+
+/* Human-readable blst-style name for a status code ("BLST_INVALID_SIZE", ...). */
+const char* lb_error_name(int32_t code);
+
+/* ABI version (bumped on incompatible changes). */
+int32_t lb_abi_version(void);
+
+/* One engine per GPU (one process per GPU in multi-GPU runs).  device < 0 = current. */
+int32_t lb_engine_create(int32_t device, lb_engine** out);
+void lb_engine_destroy(lb_engine* e);
+
+/*
+ * Upload one batch of jobs into device memory (copies; the caller keeps its buffers).
+ *   n_jobs        number of jobs (one job = one BlsWorkReq / one verifySignatureSets chunk)
+ *   job_offsets   n_jobs+1 prefix sums over sets (job j = sets [job_offsets[j], job_offsets[j+1]))
+ *   set_pk_offsets n_sets+1 prefix sums over pubkeys (set i aggregates pubkeys
+ *                 [set_pk_offsets[i], set_pk_offsets[i+1]); a `single` set has exactly one)
+ *   pubkeys       set_pk_offsets[n_sets] x 96 B
+ *   signing_roots n_sets x 32 B
+ *   signatures    n_sets x 96 B
+ *   sig_sizes     optional n_sets original signature byte lengths (NULL = all 96); a set whose
+ *                 length is not 96 makes its job reject with LB_INVALID_SIZE
+ */
+int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                        const uint32_t* set_pk_offsets, const uint8_t* pubkeys,
+                        const uint8_t* signing_roots, const uint8_t* signatures,
+                        const uint32_t* sig_sizes, lb_batch** out);
+void lb_batch_destroy(lb_batch* b);
+uint32_t lb_batch_num_sets(const lb_batch* b);
+uint32_t lb_batch_num_jobs(const lb_batch* b);
+
+/*
+ * Verify a resident batch: out_job[n_jobs] receives 1 / 0 / -code per job.
+ * scalars: n_sets non-zero 64-bit blinding scalars, or NULL to draw them from the OS
+ * CSPRNG (getrandom), as blst's verifyMultipleSignatures draws 8 random bytes per set.
+ * All valid jobs are checked with ONE final exponentiation; a failing batch is bisected
+ * over a product tree of jobs down to the invalid ones.
+ */
+int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* scalars, int32_t* out_job);
+
+/*
+ * Multi-GPU split.  lb_batch_partial runs the batch up to its root partial product
+ *   f = prod_i ML(r_i PK_i, H(m_i)) * ML(-G1, sum_i r_i sig_i)        (576 B, see above)
+ * and per-job error codes (out_job: -code for rejecting jobs, 1 otherwise).
+ * lb_fp12_product_is_one multiplies n such partials and runs one final exponentiation;
+ * *ok = 1 iff the product is 1 in GT (every valid job of every partial verifies).
+ * On a 0 verdict, call lb_batch_verify on each shard to localise the invalid jobs.
+ */
+int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint8_t* out576,
+                         int32_t* out_job);
+int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials576, uint32_t n, int32_t* ok);
+
+/* upload + verify + free in one call */
+int32_t lb_verify_jobs(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                       const uint32_t* set_pk_offsets, const uint8_t* pubkeys,
+                       const uint8_t* signing_roots, const uint8_t* signatures,
+                       const uint32_t* sig_sizes, const uint64_t* scalars, int32_t* out_job);
+
+/*
+ * G1 pubkey aggregation (getAggregatedPubkey + toBytes(uncompressed)):
+ * out96[n_sets x 96] = ZCash uncompressed sum of each set's pubkeys; out_status[n_sets]
+ * = LB_OK or the error (bad encoding / not on curve / LB_EMPTY_AGGREGATE_ARRAY).
+ */
+int32_t lb_aggregate_pubkeys(lb_engine* e, uint32_t n_sets, const uint32_t* set_pk_offsets,
+                             const uint8_t* pubkeys, uint8_t* out96, int32_t* out_status);
+
+/*
+ * Batch G1 decompression (48 B compressed -> 96 B uncompressed), the pubkey cache's one-time
+ * deserialisation (state-transition/src/cache/pubkeyCache.ts:56-77).  validate != 0 adds
+ * PublicKey.keyValidate: infinity -> LB_PK_IS_INFINITY, not in G1 -> LB_POINT_NOT_IN_GROUP.
+ */
+int32_t lb_g1_decompress(lb_engine* e, uint32_t n, const uint8_t* in48, uint8_t* out96, int32_t* out_status,
+                         int32_t validate);
+
+/*
+ * Synthetic-data helpers for tests and the benchmark (not on the verification path):
+ * SecretKey.toPublicKey and SecretKey.sign as used by the reference's own tests
+ * (test/e2e/chain/bls/multithread.test.ts:28-31).  Secret keys are 32-byte big-endian < r.
+ */
+int32_t lb_sk_to_pk(lb_engine* e, uint32_t n, const uint8_t* sks32, uint8_t* out48, uint8_t* out96);
+int32_t lb_sign(lb_engine* e, uint32_t n, const uint8_t* sks32, const uint8_t* msgs32, uint8_t* out96);
+
+/*
+ * Per-stage device timings of the last lb_batch_verify / lb_batch_partial on this engine,
+ * measured with HIP events on the engine's stream.  names[i] / ms[i] for i < *n (max cap).
+ */
+int32_t lb_engine_set_profiling(lb_engine* e, int32_t enable);
+int32_t lb_engine_last_profile(lb_engine* e, const char** names, float* ms, int32_t cap, int32_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LODESTAR_BLS_H */

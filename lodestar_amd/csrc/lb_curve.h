@@ -48,7 +48,7 @@ LB_HD jac<F> jac_neg(const jac<F>& p) {
 
 // dbl-2009-l
 template <class F>
-LB_HD jac<F> jac_dbl(const jac<F>& p) {
+LB_NI jac<F> jac_dbl(jac<F> p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -64,7 +64,7 @@ LB_HD jac<F> jac_dbl(const jac<F>& p) {
 
 // add-2007-bl with the exceptional cases handled
 template <class F>
-LB_HD jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
+LB_NI jac<F> jac_add(jac<F> p, jac<F> q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.z);
@@ -91,7 +91,7 @@ LB_HD jac<F> jac_add(const jac<F>& p, const jac<F>& q) {
 
 // madd-2007-bl: p Jacobian + q affine (q not infinity)
 template <class F>
-LB_HD jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
+LB_NI jac<F> jac_add_aff(jac<F> p, aff<F> q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.z);
   F U2 = f_mul(q.x, Z1Z1);
@@ -114,7 +114,7 @@ LB_HD jac<F> jac_add_aff(const jac<F>& p, const aff<F>& q) {
 }
 
 template <class F>
-LB_HD bool jac_eq(const jac<F>& p, const jac<F>& q) {
+LB_NI bool jac_eq(jac<F> p, jac<F> q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F Z1Z1 = f_sqr(p.z), Z2Z2 = f_sqr(q.z);
@@ -124,7 +124,7 @@ LB_HD bool jac_eq(const jac<F>& p, const jac<F>& q) {
 
 // to affine; returns false for infinity
 template <class F>
-LB_HD bool jac_to_aff(aff<F>& out, const jac<F>& p) {
+LB_NI bool jac_to_aff(aff<F>& out, jac<F> p) {
   F zi = f_inv(p.z);
   F zi2 = f_sqr(zi);
   out.x = f_mul(p.x, zi2);
@@ -134,7 +134,7 @@ LB_HD bool jac_to_aff(aff<F>& out, const jac<F>& p) {
 
 // [k]P for a 64-bit scalar, P affine (left-to-right double-and-add)
 template <class F>
-LB_HD jac<F> jac_mul_u64(const aff<F>& p, uint64_t k) {
+LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 63; i >= 0; i--) {
     acc = jac_dbl(acc);
@@ -143,9 +143,32 @@ LB_HD jac<F> jac_mul_u64(const aff<F>& p, uint64_t k) {
   return acc;
 }
 
+// [k]P for a 64-bit scalar, P Jacobian (used after aggregation, before the one inversion)
+template <class F>
+LB_NI jac<F> jac_mul_u64_jac(jac<F> p, uint64_t k) {
+  jac<F> acc = jac_infinity<F>();
+  for (int i = 63; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((k >> i) & 1ull) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+// [k]P for a 256-bit scalar (8 little-endian u32 words), P affine.  Synthetic-data helper
+// (SecretKey.toPublicKey / SecretKey.sign), not on the verification path.
+template <class F>
+LB_NI jac<F> jac_mul_u256(aff<F> p, const uint32_t* k) {
+  jac<F> acc = jac_infinity<F>();
+  for (int i = 255; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff(acc, p);
+  }
+  return acc;
+}
+
 // [|x|]P for the curve parameter |x| = 0xd201000000010000 (wave-uniform bits)
 template <class F>
-LB_HD jac<F> jac_mul_xabs(const jac<F>& p) {
+LB_NI jac<F> jac_mul_xabs(jac<F> p) {
   jac<F> acc = p;  // top bit
   for (int i = 62; i >= 0; i--) {
     acc = jac_dbl(acc);
@@ -178,7 +201,7 @@ LB_HD bool g2_in_subgroup(const g2j& p) {
 }
 
 // h_eff * P via psi (RFC 9380 App. G.3 / Budroni-Pintore)
-LB_HD g2j g2_clear_cofactor(const g2j& p) {
+LB_NI g2j g2_clear_cofactor(g2j p) {
   g2j t1 = jac_neg(jac_mul_xabs(p));  // [x]P
   g2j t2 = g2_psi(p);
   g2j t3 = g2_psi2(jac_dbl(p));

@@ -108,7 +108,10 @@ LB_HD fp fp_neg(const fp& a) { return fp_sub(fp_zero(), a); }
 LB_HD fp fp_dbl(const fp& a) { return fp_add(a, a); }
 
 // Montgomery multiplication, CIOS with 32-bit limbs: a*b/R mod p.
-LB_HD fp fp_mul(const fp& a, const fp& b) {
+// Not inlined on the GPU: one ~450-instruction body shared by every call site keeps the
+// pipeline kernels inside the instruction cache (a fully inlined Miller loop is >1 MB of
+// code) and keeps compile time bounded.  Arguments travel in VGPRs (2 x 12 words).
+LB_NI fp fp_mul(fp a, fp b) {
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
   uint32_t t[14];
   LB_UNROLL for (int j = 0; j < 14; j++) t[j] = 0;
@@ -150,7 +153,7 @@ LB_HD fp fp_from_mont(const fp& a) {
 
 // a^e for a compile-time-constant exponent held in (constant) memory; the exponent
 // bits are wave-uniform so the branch is a scalar branch on the GPU.
-LB_HD fp fp_pow_const(const fp& a, const uint32_t* e, int top_bit) {
+LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) {
   fp r = a;
   for (int i = top_bit - 1; i >= 0; i--) {
     r = fp_sqr(r);
@@ -221,21 +224,35 @@ LB_HD fp2 fp2_mul3(const fp2& a) { return fp2{fp_mul3(a.c0), fp_mul3(a.c1)}; }
 LB_HD fp2 fp2_mul4(const fp2& a) { return fp2{fp_mul4(a.c0), fp_mul4(a.c1)}; }
 LB_HD fp2 fp2_mul8(const fp2& a) { return fp2{fp_mul8(a.c0), fp_mul8(a.c1)}; }
 
-LB_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
+// Tower layers above Fp are out-of-line with pointer arguments (values live in the
+// caller's frame); only fp_mul's operands travel in registers.
+LB_NI void fp2_mul_p(fp2* r, const fp2* pa, const fp2* pb) {
+  fp2 a = *pa, b = *pb;
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
   fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+  *r = fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
-LB_HD fp2 fp2_sqr(const fp2& a) {
+LB_NI void fp2_sqr_p(fp2* r, const fp2* pa) {
+  fp2 a = *pa;
   fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
   fp t1 = fp_mul(a.c0, a.c1);
-  return fp2{t0, fp_dbl(t1)};
+  *r = fp2{t0, fp_dbl(t1)};
+}
+LB_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp2 r;
+  fp2_mul_p(&r, &a, &b);
+  return r;
+}
+LB_HD fp2 fp2_sqr(const fp2& a) {
+  fp2 r;
+  fp2_sqr_p(&r, &a);
+  return r;
 }
 // multiply by the non-residue xi = 1 + u
 LB_HD fp2 fp2_mul_xi(const fp2& a) { return fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 
-LB_HD fp2 fp2_inv(const fp2& a) {
+LB_NI fp2 fp2_inv(fp2 a) {
   fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp ni = fp_inv(n);
   return fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
@@ -245,7 +262,7 @@ LB_HD bool fp2_is_square(const fp2& a) { return fp_is_square(fp_add(fp_sqr(a.c0)
 
 // Square root in Fp2 by the complex method (p = 3 mod 4): three Fp exponentiations,
 // no data-dependent branches.  Returns true iff a is a square; `out` is some root.
-LB_HD bool fp2_sqrt(fp2& out, const fp2& a) {
+LB_NI bool fp2_sqrt(fp2& out, fp2 a) {
   fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
   fp inv2 = fp_load(LB_INV2);
@@ -286,14 +303,21 @@ LB_HD fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6{fp2_sub(a.c0, b.c0), 
 LB_HD fp6 fp6_neg(const fp6& a) { return fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 LB_HD fp6 fp6_mul_v(const fp6& a) { return fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
-LB_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
+LB_NI void fp6_mul_p(fp6* r, const fp6* pa, const fp6* pb) {
+  const fp6& a = *pa;
+  const fp6& b = *pb;
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
   fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
   fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
   fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
-  return fp6{c0, c1, c2};
+  *r = fp6{c0, c1, c2};
+}
+LB_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
+  fp6 r;
+  fp6_mul_p(&r, &a, &b);
+  return r;
 }
 
 // a * (b0 + b1 v)  (sparse: c2 coefficient zero)
@@ -311,7 +335,7 @@ LB_HD fp6 fp6_mul_1(const fp6& a, const fp2& b1) {
   return fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
 }
 
-LB_HD fp6 fp6_inv(const fp6& a) {
+LB_NI fp6 fp6_inv(fp6 a) {
   fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -328,32 +352,52 @@ LB_HD bool fp12_is_one(const fp12& a) {
 }
 LB_HD fp12 fp12_conj(const fp12& a) { return fp12{a.c0, fp6_neg(a.c1)}; }
 
-LB_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
+LB_NI void fp12_mul_p(fp12* r, const fp12* pa, const fp12* pb) {
+  const fp12& a = *pa;
+  const fp12& b = *pb;
   fp6 t0 = fp6_mul(a.c0, b.c0);
   fp6 t1 = fp6_mul(a.c1, b.c1);
   fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
-  return fp12{c0, c1};
+  *r = fp12{c0, c1};
+}
+LB_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
+  fp12 r;
+  fp12_mul_p(&r, &a, &b);
+  return r;
 }
 
-LB_HD fp12 fp12_sqr(const fp12& a) {
+LB_NI void fp12_sqr_p(fp12* r, const fp12* pa) {
   // complex squaring: (a0 + a1 w)^2 = a0^2 + v a1^2 + 2 a0 a1 w
+  const fp12& a = *pa;
   fp6 t = fp6_mul(a.c0, a.c1);
   fp6 c0 = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   c0 = fp6_sub(fp6_sub(c0, t), fp6_mul_v(t));
-  return fp12{c0, fp6_add(t, t)};
+  *r = fp12{c0, fp6_add(t, t)};
+}
+LB_HD fp12 fp12_sqr(const fp12& a) {
+  fp12 r;
+  fp12_sqr_p(&r, &a);
+  return r;
 }
 
 // multiply by a Miller-loop line  l = (l0 + l2 v) + (l3 v) w   (w-basis: l0 w^0 + l2 w^2 + l3 w^3)
-LB_HD fp12 fp12_mul_line(const fp12& a, const fp2& l0, const fp2& l2, const fp2& l3) {
+LB_NI void fp12_mul_line_p(fp12* r, const fp12* pa, const fp2* pl0, const fp2* pl2, const fp2* pl3) {
+  const fp12& a = *pa;
+  const fp2 &l0 = *pl0, &l2 = *pl2, &l3 = *pl3;
   fp6 t0 = fp6_mul_01(a.c0, l0, l2);
   fp6 t1 = fp6_mul_1(a.c1, l3);
   fp6 c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(a.c0, a.c1), l0, fp2_add(l2, l3)), t0), t1);
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
-  return fp12{c0, c1};
+  *r = fp12{c0, c1};
+}
+LB_HD fp12 fp12_mul_line(const fp12& a, const fp2& l0, const fp2& l2, const fp2& l3) {
+  fp12 r;
+  fp12_mul_line_p(&r, &a, &l0, &l2, &l3);
+  return r;
 }
 
-LB_HD fp12 fp12_inv(const fp12& a) {
+LB_NI fp12 fp12_inv(fp12 a) {
   fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
   fp6 ti = fp6_inv(t);
   return fp12{fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti))};
@@ -361,7 +405,7 @@ LB_HD fp12 fp12_inv(const fp12& a) {
 
 // Frobenius a -> a^p.  In the w-basis a = sum a_k w^k (a_0=c0.c0, a_1=c1.c0, a_2=c0.c1,
 // a_3=c1.c1, a_4=c0.c2, a_5=c1.c2), a^p = sum conj(a_k) xi^(k(p-1)/6) w^k.
-LB_HD fp12 fp12_frob(const fp12& a) {
+LB_NI fp12 fp12_frob(fp12 a) {
   fp12 r;
   r.c0.c0 = fp2_conj(a.c0.c0);
   r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), fp2_load(LB_FROB1_1));
@@ -371,7 +415,7 @@ LB_HD fp12 fp12_frob(const fp12& a) {
   r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), fp2_load(LB_FROB1_5));
   return r;
 }
-LB_HD fp12 fp12_frob2(const fp12& a) {
+LB_NI fp12 fp12_frob2(fp12 a) {
   fp12 r;
   r.c0.c0 = a.c0.c0;
   r.c1.c0 = fp2_mul_fp(a.c1.c0, fp_load(LB_FROB2_1));

@@ -20,7 +20,7 @@ LB_CONST uint32_t LB_SHA_K[64] = {
 LB_HD uint32_t lb_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
 // one compression of a 16-word big-endian block into state h
-LB_HD void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
+LB_NI void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
   uint32_t w[16];
   LB_UNROLL for (int i = 0; i < 16; i++) w[i] = blk[i];
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
@@ -111,7 +111,7 @@ LB_HD void sha256_small(uint32_t out[8], const uint8_t* m, int len, bool zero_bl
 }
 
 // expand_message_xmd(msg32, DST, 256) -> 8 x 32-byte blocks (as big-endian words)
-LB_HD void expand_message_xmd_256(uint32_t out[64], const uint8_t msg[32]) {
+LB_NI void expand_message_xmd_256(uint32_t out[64], const uint8_t msg[32]) {
   uint8_t buf[32 + 2 + 1 + LB_DST_LEN + 1];
   // b0 = H(Z_pad || msg || I2OSP(256, 2) || I2OSP(0, 1) || DST')
   for (int i = 0; i < 32; i++) buf[i] = msg[i];
@@ -160,7 +160,7 @@ LB_HD fp fp_from_be64_words(const uint32_t* wds) {
 }
 
 // ------------------------------------------------------------------ SSWU + 3-isogeny
-LB_HD g2j map_to_curve_g2(const fp2& u) {
+LB_NI g2j map_to_curve_g2(fp2 u) {
   const fp2 A = fp2_load(LB_SSWU_A), B = fp2_load(LB_SSWU_B), Z = fp2_load(LB_SSWU_Z);
   fp2 u2 = fp2_sqr(u);
   fp2 zu2 = fp2_mul(Z, u2);

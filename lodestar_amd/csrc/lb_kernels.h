@@ -1,0 +1,372 @@
+// gfx950 kernels of the signature-set verification pipeline (one thread per work item).
+//
+// Pipeline for one batch of jobs (blst semantics of
+// Pairing.mul_n_aggregate + commit + finalverify behind maybeBatch.ts:18-25):
+//   k_decode_sigs     per set   : compressed G2 -> affine + subgroup check   (Signature.fromBytes(.., true))
+//   k_hash_map        per set x2: expand_message_xmd + SSWU + 3-isogeny      (hash_to_G2, first half)
+//   k_hash_finish     per set   : Q0 + Q1, clear cofactor, to affine          (hash_to_G2, second half)
+//   k_pk_blind        per set   : G1 aggregation (utils.ts:5-16), r*PK, r*sig
+//   k_miller          per set   : ML(r*PK, H(m))                               (Pairing.mul_n_aggregate)
+//   k_job_leaves      per job   : P_j = prod ML, S_j = sum r*sig -> tree leaves
+//   k_tree_up         per node  : product tree over jobs (bisection structure)
+//   k_node_check      per node  : FE(P * ML(-G1, S)) == 1                      (Pairing.finalverify)
+// All intermediate arrays are structure-of-arrays, word-major: word w of element e lives at
+// base[w * n + e], so a wave's 64 lanes touch 64 consecutive words per access.
+#pragma once
+#include "lb_serial.h"
+#include "lb_h2c.h"
+#include "lb_pairing.h"
+
+#define LB_TPB 64  // one wave per workgroup: spreads few-thousand-item batches over all 256 CUs
+
+template <class T>
+__device__ __forceinline__ T soa_ld(const uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized types only");
+  T r;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); i++) w[i] = base[(size_t)i * n + e];
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void soa_st(uint32_t* __restrict__ base, uint32_t n, uint32_t e, const T& v) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); i++) base[(size_t)i * n + e] = w[i];
+}
+
+template <int N>
+__device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict__ src) {
+  static_assert(N % 16 == 0, "16-byte multiples");
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int i = 0; i < N / 16; i++) {
+    uint4 v = s[i];
+    uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      dst[16 * i + 4 * k + 0] = (uint8_t)ws[k];
+      dst[16 * i + 4 * k + 1] = (uint8_t)(ws[k] >> 8);
+      dst[16 * i + 4 * k + 2] = (uint8_t)(ws[k] >> 16);
+      dst[16 * i + 4 * k + 3] = (uint8_t)(ws[k] >> 24);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ---------------------------------------------------------------- signatures
+// sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
+__global__ void __launch_bounds__(LB_TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                        const uint32_t* __restrict__ sig_sizes,
+                                                        uint32_t* __restrict__ sig_aff,
+                                                        uint32_t* __restrict__ sig_inf,
+                                                        int32_t* __restrict__ sig_status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  int st = LB_OK;
+  g2a a;
+  bool inf = false;
+  if (sig_sizes != nullptr && sig_sizes[i] != 96) {
+    st = LB_INVALID_SIZE;
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    uint8_t b[96];
+    ld_bytes<96>(b, sigs + (size_t)96 * i);
+    st = g2_decompress96(b, a, inf);
+    if (st == LB_OK && !inf && !g2_in_subgroup(jac_from_aff(a))) st = LB_POINT_NOT_IN_GROUP;
+  }
+  soa_st(sig_aff, n, i, a);
+  sig_inf[i] = inf ? 1u : 0u;
+  sig_status[i] = st;
+}
+
+// ---------------------------------------------------------------- hash_to_G2
+// thread t: set t % n, field element u_{t / n}; output Jacobian points q[2n]
+__global__ void __launch_bounds__(LB_TPB) k_hash_map(uint32_t n, const uint8_t* __restrict__ msgs,
+                                                     uint32_t* __restrict__ q) {
+  uint32_t t = lb_tid();
+  if (t >= 2 * n) return;
+  uint32_t i = t < n ? t : t - n;
+  uint32_t which = t < n ? 0u : 1u;
+  uint8_t m[32];
+  ld_bytes<32>(m, msgs + (size_t)32 * i);
+  uint32_t ub[64];
+  expand_message_xmd_256(ub, m);
+  const uint32_t* w = ub + 32 * which;
+  fp2 u{fp_from_be64_words(w), fp_from_be64_words(w + 16)};
+  g2j p = map_to_curve_g2(u);
+  soa_st(q, 2 * n, t, p);
+}
+
+__global__ void __launch_bounds__(LB_TPB) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
+                                                        uint32_t* __restrict__ h_aff) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  g2j q0 = soa_ld<g2j>(q, 2 * n, i);
+  g2j q1 = soa_ld<g2j>(q, 2 * n, n + i);
+  g2j h = g2_clear_cofactor(jac_add(q0, q1));
+  g2a a;
+  jac_to_aff(a, h);  // H(m) == infinity has negligible probability; its z=0 gives x=y=0
+  soa_st(h_aff, n, i, a);
+}
+
+// ---------------------------------------------------------------- pubkeys + blinding
+// pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
+__global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, const uint32_t* __restrict__ pk_off,
+                                                     const uint8_t* __restrict__ pks,
+                                                     const uint64_t* __restrict__ scalars,
+                                                     const uint32_t* __restrict__ sig_aff,
+                                                     const uint32_t* __restrict__ sig_inf,
+                                                     const int32_t* __restrict__ sig_status,
+                                                     uint32_t* __restrict__ rpk_aff,
+                                                     uint32_t* __restrict__ rsig,
+                                                     int32_t* __restrict__ pk_status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t a = pk_off[i], e = pk_off[i + 1];
+  int st = (a == e) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+  g1j acc = jac_infinity<fp>();
+  bool single = (e - a) == 1;
+  g1a first;
+  for (uint32_t k = a; k < e && st == LB_OK; k++) {
+    uint8_t b[96];
+    ld_bytes<96>(b, pks + (size_t)96 * k);
+    g1a p;
+    bool inf;
+    st = g1_deserialize96(b, p, inf);
+    if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+    if (k == a) first = p;
+  }
+  if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
+  uint64_t r = scalars[i];
+  g1a rp;
+  rp.x = fp_zero();
+  rp.y = fp_zero();
+  g2j rs = jac_infinity<fp2>();
+  if (st == LB_OK) {
+    g1j rj = single ? jac_mul_u64(first, r) : jac_mul_u64_jac(acc, r);
+    jac_to_aff(rp, rj);
+    if (sig_status[i] == LB_OK && sig_inf[i] == 0u) rs = jac_mul_u64(soa_ld<g2a>(sig_aff, n, i), r);
+  }
+  soa_st(rpk_aff, n, i, rp);
+  soa_st(rsig, n, i, rs);
+  pk_status[i] = st;
+}
+
+// ---------------------------------------------------------------- Miller loops
+__global__ void __launch_bounds__(LB_TPB) k_miller(uint32_t n, const uint32_t* __restrict__ rpk_aff,
+                                                   const uint32_t* __restrict__ h_aff,
+                                                   const int32_t* __restrict__ sig_status,
+                                                   const int32_t* __restrict__ pk_status,
+                                                   uint32_t* __restrict__ ml) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  fp12 f = fp12_one();
+  if (sig_status[i] == LB_OK && pk_status[i] == LB_OK) {
+    g1a p = soa_ld<g1a>(rpk_aff, n, i);
+    g2a h = soa_ld<g2a>(h_aff, n, i);
+    f = miller_loop(p, h);
+  }
+  soa_st(ml, n, i, f);
+}
+
+// ---------------------------------------------------------------- per-job leaves
+// Job status follows maybeBatch.ts: all signatures are decoded first (first failing one
+// throws), then pubkeys are consumed in order by mul_n_aggregate.
+__global__ void __launch_bounds__(LB_TPB) k_job_leaves(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
+                                                       const uint32_t* __restrict__ job_off,
+                                                       const int32_t* __restrict__ sig_status,
+                                                       const int32_t* __restrict__ pk_status,
+                                                       const uint32_t* __restrict__ ml,
+                                                       const uint32_t* __restrict__ rsig,
+                                                       uint32_t* __restrict__ treeP,
+                                                       uint32_t* __restrict__ treeS,
+                                                       int32_t* __restrict__ job_status) {
+  uint32_t j = lb_tid();
+  if (j >= m) return;
+  fp12 P = fp12_one();
+  g2j S = jac_infinity<fp2>();
+  int st = LB_OK;
+  if (j < n_jobs) {
+    uint32_t a = job_off[j], e = job_off[j + 1];
+    // error precedence of the reference: aggregation / pubkey decoding happen first
+    // (main thread getAggregatedPubkey, worker deserializeSet), then every signature is
+    // decoded (maybeBatch.ts:18-25), then mul_n_aggregate rejects an infinite pubkey.
+    if (a == e) st = LB_EMPTY_SIGNATURE_SET;
+    for (uint32_t i = a; i < e && st == LB_OK; i++)
+      if (pk_status[i] != LB_OK && pk_status[i] != LB_PK_IS_INFINITY) st = pk_status[i];
+    for (uint32_t i = a; i < e && st == LB_OK; i++)
+      if (sig_status[i] != LB_OK) st = sig_status[i];
+    for (uint32_t i = a; i < e && st == LB_OK; i++)
+      if (pk_status[i] != LB_OK) st = pk_status[i];
+    if (st == LB_OK) {
+      for (uint32_t i = a; i < e; i++) {
+        fp12 f = soa_ld<fp12>(ml, n_sets, i);
+        P = (i == a) ? f : fp12_mul(P, f);
+        S = jac_add(S, soa_ld<g2j>(rsig, n_sets, i));
+      }
+    }
+    job_status[j] = st;
+  }
+  if (st != LB_OK) {
+    P = fp12_one();
+    S = jac_infinity<fp2>();
+  }
+  soa_st(treeP, 2 * m, m + j, P);
+  soa_st(treeS, 2 * m, m + j, S);
+}
+
+// nodes [lo, 2 lo): node i = node 2i (x) node 2i+1
+__global__ void __launch_bounds__(LB_TPB) k_tree_up(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP,
+                                                    uint32_t* __restrict__ treeS) {
+  uint32_t t = lb_tid();
+  if (t >= lo) return;
+  uint32_t i = lo + t;
+  fp12 a = soa_ld<fp12>(treeP, 2 * m, 2 * i), b = soa_ld<fp12>(treeP, 2 * m, 2 * i + 1);
+  soa_st(treeP, 2 * m, i, fp12_mul(a, b));
+  g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
+  soa_st(treeS, 2 * m, i, s);
+}
+
+// f = P * ML(-G1, S)
+__device__ __forceinline__ fp12 node_partial(const fp12& P, const g2j& S) {
+  if (jac_is_inf(S)) return P;
+  g2a sa;
+  jac_to_aff(sa, S);
+  g1a ng1{fp_load(LB_G1X), fp_load(LB_G1NEGY)};
+  return fp12_mul(P, miller_loop(ng1, sa));
+}
+
+__global__ void __launch_bounds__(LB_TPB) k_node_check(uint32_t m, uint32_t cnt, const uint32_t* __restrict__ nodes,
+                                                       const uint32_t* __restrict__ treeP,
+                                                       const uint32_t* __restrict__ treeS,
+                                                       int32_t* __restrict__ verdict) {
+  uint32_t t = lb_tid();
+  if (t >= cnt) return;
+  uint32_t i = nodes[t];
+  fp12 f = node_partial(soa_ld<fp12>(treeP, 2 * m, i), soa_ld<g2j>(treeS, 2 * m, i));
+  verdict[t] = fp12_is_one(final_exponentiation(f)) ? 1 : 0;
+}
+
+// root partial product as 576 bytes (multi-GPU exchange format)
+__global__ void __launch_bounds__(LB_TPB) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                         const uint32_t* __restrict__ treeS,
+                                                         uint8_t* __restrict__ out576) {
+  if (lb_tid() != 0) return;
+  fp12 f = node_partial(soa_ld<fp12>(treeP, 2 * m, 1), soa_ld<g2j>(treeS, 2 * m, 1));
+  fp12_to_be576(out576, f);
+}
+
+__global__ void __launch_bounds__(LB_TPB) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
+                                                           int32_t* __restrict__ ok) {
+  if (lb_tid() != 0) return;
+  fp12 acc = fp12_one();
+  bool good = true;
+  for (uint32_t i = 0; i < n; i++) {
+    fp12 f;
+    good &= fp12_from_be576(f, parts + (size_t)576 * i);
+    acc = fp12_mul(acc, f);
+  }
+  *ok = (good && fp12_is_one(final_exponentiation(acc))) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- pubkey aggregation only
+__global__ void __launch_bounds__(LB_TPB) k_aggregate(uint32_t n, const uint32_t* __restrict__ pk_off,
+                                                      const uint8_t* __restrict__ pks, uint8_t* __restrict__ out96,
+                                                      int32_t* __restrict__ status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t a = pk_off[i], e = pk_off[i + 1];
+  int st = (a == e) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+  g1j acc = jac_infinity<fp>();
+  for (uint32_t k = a; k < e && st == LB_OK; k++) {
+    uint8_t b[96];
+    ld_bytes<96>(b, pks + (size_t)96 * k);
+    g1a p;
+    bool inf;
+    st = g1_deserialize96(b, p, inf);
+    if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+  }
+  uint8_t ob[96];
+  g1a r;
+  bool fin = jac_to_aff(r, acc);
+  g1_serialize96(ob, r, !fin || st != LB_OK);
+  for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
+  status[i] = st;
+}
+
+// ---------------------------------------------------------------- G1 decompression
+// 48-byte compressed pubkeys -> 96-byte uncompressed (the pubkey cache's one-time
+// deserialisation, state-transition/src/cache/pubkeyCache.ts:56-77).  validate = subgroup
+// + infinity check (PublicKey.keyValidate).
+__global__ void __launch_bounds__(LB_TPB) k_g1_decompress(uint32_t n, const uint8_t* __restrict__ in48,
+                                                          uint8_t* __restrict__ out96, int32_t* __restrict__ status,
+                                                          int32_t validate) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint8_t b[48];
+  ld_bytes<48>(b, in48 + (size_t)48 * i);
+  g1a a;
+  bool inf;
+  int st = g1_decompress48(b, a, inf);
+  if (st == LB_OK && validate) {
+    if (inf) {
+      st = LB_PK_IS_INFINITY;
+    } else {
+      // r * P == O  (r = BLS12-381 subgroup order); plain check, one-time per key
+      uint32_t rr[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                        0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+      if (!jac_is_inf(jac_mul_u256(a, rr))) st = LB_POINT_NOT_IN_GROUP;
+    }
+  }
+  uint8_t ob[96];
+  g1_serialize96(ob, a, inf || st != LB_OK);
+  for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
+  status[i] = st;
+}
+
+// ---------------------------------------------------------------- synthetic data (bench/tests)
+// sk (32-byte big-endian, < r) -> 48-byte compressed and 96-byte uncompressed pubkey
+__global__ void __launch_bounds__(LB_TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks,
+                                                     uint8_t* __restrict__ out48, uint8_t* __restrict__ out96) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int w = 0; w < 8; w++) {
+    const uint8_t* s = sks + (size_t)32 * i + 28 - 4 * w;
+    k[w] = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | s[3];
+  }
+  g1a g{fp_load(LB_G1X), fp_load(LB_G1Y)};
+  g1a a;
+  bool fin = jac_to_aff(a, jac_mul_u256(g, k));
+  uint8_t c[48], u[96];
+  g1_compress48(c, a, !fin);
+  g1_serialize96(u, a, !fin);
+  if (out48)
+    for (int j = 0; j < 48; j++) out48[(size_t)48 * i + j] = c[j];
+  if (out96)
+    for (int j = 0; j < 96; j++) out96[(size_t)96 * i + j] = u[j];
+}
+
+// sig = sk * H(m), 96-byte compressed
+__global__ void __launch_bounds__(LB_TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sks,
+                                                 const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int w = 0; w < 8; w++) {
+    const uint8_t* s = sks + (size_t)32 * i + 28 - 4 * w;
+    k[w] = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | s[3];
+  }
+  uint8_t m[32];
+  for (int j = 0; j < 32; j++) m[j] = msgs[(size_t)32 * i + j];
+  g2a h;
+  jac_to_aff(h, hash_to_g2(m));
+  g2a a;
+  bool fin = jac_to_aff(a, jac_mul_u256(h, k));
+  uint8_t c[96];
+  g2_compress96(c, a, !fin);
+  for (int j = 0; j < 96; j++) out96[(size_t)96 * i + j] = c[j];
+}

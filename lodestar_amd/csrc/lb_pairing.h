@@ -11,7 +11,7 @@
 #include "lb_curve.h"
 
 // doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P
-LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+LB_NI void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
   const fp2 b3 = fp2_load(LB_B2_3);  // 3 b'
   fp2 X = T.x, Y = T.y, Z = T.z;
   fp2 A = fp2_mul(X, Y);             // XY (halved below)
@@ -36,7 +36,7 @@ LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp&
 }
 
 // addition step T <- T + Q (Q affine), line through T and Q at P
-LB_HD void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+LB_NI void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
   fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
   // line: (theta xQ - lam yQ) + (-theta xP) w^2 + (lam yP) w^3
@@ -55,7 +55,7 @@ LB_HD void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp&
 }
 
 // f_{|x|,Q}(P), conjugated (x < 0).  P, Q affine and not infinity.
-LB_HD fp12 miller_loop(const g1a& P, const g2a& Q) {
+LB_NI fp12 miller_loop(g1a P, g2a Q) {
   g2j T;
   T.x = Q.x;
   T.y = Q.y;
@@ -80,7 +80,7 @@ LB_HD fp12 miller_loop(const g1a& P, const g2a& Q) {
 }
 
 // a^|x| for a in the cyclotomic subgroup
-LB_HD fp12 fp12_pow_xabs(const fp12& a) {
+LB_NI fp12 fp12_pow_xabs(fp12 a) {
   fp12 r = a;
   for (int i = 62; i >= 0; i--) {
     r = fp12_sqr(r);
@@ -90,7 +90,7 @@ LB_HD fp12 fp12_pow_xabs(const fp12& a) {
 }
 
 // f^(3 (p^12 - 1)/r)
-LB_HD fp12 final_exponentiation(const fp12& f) {
+LB_NI fp12 final_exponentiation(fp12 f) {
   // easy part: f^((p^6 - 1)(p^2 + 1))
   fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));
   t = fp12_mul(fp12_frob2(t), t);

@@ -155,3 +155,17 @@ LB_HD void fp12_to_be576(uint8_t* b, const fp12& a) {
     fp_plain_to_be48(b + 96 * i + 48, fp_from_mont(parts[i]->c1));
   }
 }
+
+// 576 bytes (layout of fp12_to_be576) -> Fp12; false if a coefficient is >= p
+LB_HD bool fp12_from_be576(fp12& a, const uint8_t* b) {
+  fp2* parts[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  bool ok = true;
+  for (int i = 0; i < 6; i++) {
+    fp x0, x1;
+    ok &= fp_plain_from_be48(x0, b + 96 * i, 0xff);
+    ok &= fp_plain_from_be48(x1, b + 96 * i + 48, 0xff);
+    parts[i]->c0 = fp_to_mont(x0);
+    parts[i]->c1 = fp_to_mont(x1);
+  }
+  return ok;
+}

@@ -1,0 +1,250 @@
+"""Host-side mirror of Lodestar's IBlsVerifier over the MI355X engine.
+
+Reference interface and policy (paths under the reference repo):
+  * IBlsVerifier / VerifySignatureOpts     packages/beacon-node/src/chain/bls/interface.ts:3-46
+  * BlsMultiThreadWorkerPool policy        packages/beacon-node/src/chain/bls/multithread/index.ts:98-424
+      - calls split into jobs of >=128 sets (chunkifyMaximizeChunkSize, :39,156; utils.ts:4-19)
+      - batchable jobs buffered until >32 sigs or 100 ms (:48,57,257-275)
+      - non-batchable jobs run on the next tick (:280-283)
+      - verifyOnMainThread runs synchronously on the caller's thread (:138-151)
+      - close() rejects queued jobs with QUEUE_ABORTED (:176-197)
+  * per-job results (worker.ts:32-108): job j resolves true/false or rejects with its error,
+    independently of every other job in the same batch (multithread.test.ts:86-103).
+
+The worker threads are replaced by one GPU runner thread per engine: it drains every queued
+job into ONE device batch (one final exponentiation for all valid jobs, bisection over a
+job product tree when it fails), instead of the reference's packages of ~128 sets per CPU
+worker and per-job re-verification.
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+import time
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import List, Optional, Sequence, Union
+
+from .engine import BlsError, Engine, SetInput
+
+MAX_SIGNATURE_SETS_PER_JOB = 128   # multithread/index.ts:39
+MAX_BUFFERED_SIGS = 32             # multithread/index.ts:48
+MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:57
+
+
+class QueueError(Exception):
+    """util/queue QueueError; code QUEUE_ABORTED after close()."""
+
+    def __init__(self, code: str = "QUEUE_ABORTED"):
+        self.code = code
+        super().__init__(code)
+
+
+def chunkify_maximize_chunk_size(arr: Sequence, min_per_chunk: int) -> List[list]:
+    """multithread/utils.ts:4-19: split into floor(n/min) chunks of ceil(n/count) items."""
+    arr = list(arr)
+    chunk_count = len(arr) // min_per_chunk
+    if chunk_count <= 1:
+        return [arr]
+    per_chunk = -(-len(arr) // chunk_count)
+    return [arr[i:i + per_chunk] for i in range(0, len(arr), per_chunk)]
+
+
+class PublicKey:
+    """A G1 public key held as its 96-byte uncompressed encoding (what the reference's main
+    thread sends to workers: getAggregatedPubkey(s).toBytes(uncompressed))."""
+
+    __slots__ = ("raw",)
+
+    def __init__(self, raw96: bytes):
+        if len(raw96) != 96:
+            raise ValueError("PublicKey expects 96-byte uncompressed bytes")
+        self.raw = bytes(raw96)
+
+    @staticmethod
+    def many_from_compressed(engine: Engine, pks48: Sequence[bytes], validate: bool = False) -> List["PublicKey"]:
+        out, st = engine.g1_decompress(pks48, validate)
+        for s in st:
+            if s:
+                raise BlsError(s)
+        return [PublicKey(o) for o in out]
+
+    def to_bytes(self) -> bytes:
+        return self.raw
+
+
+class SignatureSetType(str, Enum):
+    single = "single"
+    aggregate = "aggregate"
+
+
+@dataclass
+class SingleSignatureSet:
+    pubkey: PublicKey
+    signing_root: bytes
+    signature: bytes
+    type: SignatureSetType = SignatureSetType.single
+
+
+@dataclass
+class AggregatedSignatureSet:
+    pubkeys: List[PublicKey]
+    signing_root: bytes
+    signature: bytes
+    type: SignatureSetType = SignatureSetType.aggregate
+
+
+ISignatureSet = Union[SingleSignatureSet, AggregatedSignatureSet]
+
+
+@dataclass
+class VerifySignatureOpts:
+    batchable: bool = False
+    verify_on_main_thread: bool = False
+
+
+def _to_input(s: ISignatureSet) -> SetInput:
+    if s.type == SignatureSetType.single:
+        pks = [s.pubkey.raw]
+    elif s.type == SignatureSetType.aggregate:
+        pks = [p.raw for p in s.pubkeys]
+    else:
+        raise ValueError("Unknown signature set type")
+    return SetInput(pubkeys=pks, signing_root=bytes(s.signing_root), signature=bytes(s.signature))
+
+
+def _result(code: int) -> bool:
+    if code < 0:
+        raise BlsError(-code)
+    return code == 1
+
+
+@dataclass
+class _Job:
+    sets: List[SetInput]
+    opts: VerifySignatureOpts
+    future: asyncio.Future
+    loop: asyncio.AbstractEventLoop
+    added: float = field(default_factory=time.monotonic)
+
+
+@dataclass
+class PoolStats:
+    batches: int = 0
+    jobs: int = 0
+    sets: int = 0
+    jobs_invalid: int = 0
+    jobs_error: int = 0
+
+
+class BlsGpuVerifier:
+    """IBlsVerifier backed by one MI355X engine (drop-in for BlsMultiThreadWorkerPool)."""
+
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, bls_verify_all_multi_thread: bool = False):
+        self.engine = engine if engine is not None else Engine(device)
+        self._own_engine = engine is None
+        self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
+        self.stats = PoolStats()
+        self._lock = threading.Condition()
+        self._jobs: List[_Job] = []
+        self._buffered: List[_Job] = []
+        self._buffered_sigs = 0
+        self._buffer_timer: Optional[asyncio.TimerHandle] = None
+        self._closed = False
+        self._runner = threading.Thread(target=self._run, name="lodestar-bls-gpu", daemon=True)
+        self._runner.start()
+
+    # ---------------------------------------------------------------- IBlsVerifier
+    async def verify_signature_sets(self, sets: Sequence[ISignatureSet],
+                                    opts: Optional[VerifySignatureOpts] = None) -> bool:
+        opts = opts or VerifySignatureOpts()
+        if self._closed:
+            raise QueueError("QUEUE_ABORTED")
+        inputs = [_to_input(s) for s in sets]
+        if opts.verify_on_main_thread and not self.bls_verify_all_multi_thread:
+            # synchronous, blocks the caller like the reference (multithread/index.ts:138-151)
+            return _result(self.engine.verify_jobs([inputs])[0])
+        loop = asyncio.get_running_loop()
+        futs = []
+        for chunk in chunkify_maximize_chunk_size(inputs, MAX_SIGNATURE_SETS_PER_JOB):
+            job = _Job(sets=chunk, opts=opts, future=loop.create_future(), loop=loop)
+            futs.append(job.future)
+            self._queue(job)
+        results = await asyncio.gather(*futs)
+        return all(r is True for r in results)
+
+    async def close(self) -> None:
+        with self._lock:
+            self._closed = True
+            if self._buffer_timer is not None:
+                self._buffer_timer.cancel()
+                self._buffer_timer = None
+            pending = self._jobs + self._buffered
+            self._jobs, self._buffered, self._buffered_sigs = [], [], 0
+            self._lock.notify_all()
+        for j in pending:
+            j.loop.call_soon_threadsafe(_set_exc, j.future, QueueError("QUEUE_ABORTED"))
+        await asyncio.get_running_loop().run_in_executor(None, self._runner.join)
+        if self._own_engine:
+            self.engine.close()
+
+    # ---------------------------------------------------------------- queueing policy
+    def _queue(self, job: _Job):
+        if job.opts.batchable:
+            self._buffered.append(job)
+            self._buffered_sigs += len(job.sets)
+            if self._buffered_sigs > MAX_BUFFERED_SIGS:
+                self._flush_buffer()
+            elif self._buffer_timer is None:
+                self._buffer_timer = job.loop.call_later(MAX_BUFFER_WAIT_MS / 1000.0, self._flush_buffer)
+        else:
+            with self._lock:
+                self._jobs.append(job)
+                self._lock.notify_all()
+
+    def _flush_buffer(self):
+        if self._buffer_timer is not None:
+            self._buffer_timer.cancel()
+            self._buffer_timer = None
+        with self._lock:
+            self._jobs.extend(self._buffered)
+            self._buffered, self._buffered_sigs = [], 0
+            self._lock.notify_all()
+
+    # ---------------------------------------------------------------- GPU runner
+    def _run(self):
+        while True:
+            with self._lock:
+                while not self._jobs and not self._closed:
+                    self._lock.wait()
+                if self._closed and not self._jobs:
+                    return
+                jobs, self._jobs = self._jobs, []
+            try:
+                codes = self.engine.verify_jobs([j.sets for j in jobs])
+                err = None
+            except Exception as e:  # device failure: every job of the package rejects (index.ts:368-375)
+                codes, err = None, e
+            self.stats.batches += 1
+            self.stats.jobs += len(jobs)
+            self.stats.sets += sum(len(j.sets) for j in jobs)
+            for k, j in enumerate(jobs):
+                if err is not None:
+                    j.loop.call_soon_threadsafe(_set_exc, j.future, err)
+                elif codes[k] < 0:
+                    self.stats.jobs_error += 1
+                    j.loop.call_soon_threadsafe(_set_exc, j.future, BlsError(-codes[k]))
+                else:
+                    if codes[k] == 0:
+                        self.stats.jobs_invalid += 1
+                    j.loop.call_soon_threadsafe(_set_res, j.future, codes[k] == 1)
+
+
+def _set_res(f: asyncio.Future, v):
+    if not f.done():
+        f.set_result(v)
+
+
+def _set_exc(f: asyncio.Future, e):
+    if not f.done():
+        f.set_exception(e)

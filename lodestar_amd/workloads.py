@@ -1,0 +1,148 @@
+"""Synthetic mainnet-shaped signature-set workloads (BASELINE.json configs).
+
+Keys follow the reference's perf convention: validator v uses interop key v mod 100
+(packages/state-transition/test/perf/util.ts:49-71; interop sk formula
+packages/state-transition/src/util/interop.ts:19-23).  Signing roots are
+sha256(seed || type || slot || index).  Signatures are produced on the GPU with the engine's
+synthetic-data kernels (SecretKey.sign); an aggregate signature is (sum sk_i mod r) * H(m).
+
+Shapes (jobs = verifySignatureSets calls after chunkifyMaximizeChunkSize(sets, 128)):
+  c1  128 single-pubkey sets, one job (BASELINE configs[0])
+  c2  one block: proposer + randao + 128 attestation aggregates (k=256) + sync aggregate
+      (k=358), one non-batchable call of 131 sets (configs[1])
+  c3  gossip flood per slot: 16384 attestation calls (1 set, k=1, batchable) + 1024
+      aggregate-and-proof calls (2 singles + 1 aggregate k=256)  = 17408 jobs, 19456 sets
+      (configs[2])
+  c4  sync committee: 512 single sync-committee messages + 64 contribution calls (2 singles +
+      k=128) + block sync aggregate (k=512) + 4 light-client update aggregates (k=512), with
+      one invalid set per 1000 (configs[3])
+  c5  range sync: 32 blocks of c2 shape, one call per block (configs[4])
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .engine import Engine, PackedJobs
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+SEED = 0x4C4F4445
+N_KEYS = 100
+
+
+def interop_sk(i: int) -> int:
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return int.from_bytes(d, "little") % R
+
+
+@dataclass
+class SetSpec:
+    validators: List[int]   # pubkey indices (validator ids)
+    kind: int               # domain-ish tag for the signing root
+    invalid: bool = False   # sign a different message (well-formed, wrong)
+
+
+@dataclass
+class Workload:
+    name: str
+    packed: PackedJobs
+    n_invalid_jobs: int
+    expected: np.ndarray    # per job 1 / 0
+
+
+class KeyPool:
+    def __init__(self, engine: Engine, n: int = N_KEYS):
+        self.sks = [interop_sk(i) for i in range(n)]
+        _, self.pk96 = engine.sk_to_pk(self.sks)
+
+    def sk(self, v: int) -> int:
+        return self.sks[v % len(self.sks)]
+
+    def pk(self, v: int) -> np.ndarray:
+        return self.pk96[v % len(self.sks)]
+
+
+def build(engine: Engine, jobs: Sequence[Sequence[SetSpec]], name: str, keys: Optional[KeyPool] = None,
+          seed: int = SEED) -> Workload:
+    keys = keys or KeyPool(engine)
+    flat = [s for job in jobs for s in job]
+    n = len(flat)
+    msgs = np.zeros((n, 32), dtype=np.uint8)
+    sks = []
+    for i, s in enumerate(flat):
+        msgs[i] = np.frombuffer(hashlib.sha256(seed.to_bytes(8, "little") + s.kind.to_bytes(2, "little")
+                                               + i.to_bytes(8, "little")).digest(), np.uint8)
+        sks.append(sum(keys.sk(v) for v in s.validators) % R or 1)
+    sign_msgs = msgs.copy()
+    for i, s in enumerate(flat):
+        if s.invalid:
+            sign_msgs[i, 0] ^= 0xFF
+    sigs = np.zeros((n, 96), dtype=np.uint8)
+    step = 8192
+    for a in range(0, n, step):
+        sigs[a:a + step] = engine.sign(sks[a:a + step], sign_msgs[a:a + step])
+    job_off = np.zeros(len(jobs) + 1, dtype=np.uint32)
+    job_off[1:] = np.cumsum([len(j) for j in jobs])
+    pk_off = np.zeros(n + 1, dtype=np.uint32)
+    pk_off[1:] = np.cumsum([len(s.validators) for s in flat])
+    vidx = np.fromiter((v % len(keys.sks) for s in flat for v in s.validators), dtype=np.int64)
+    pubkeys = np.ascontiguousarray(keys.pk96[vidx].reshape(-1))
+    expected = np.array([0 if any(s.invalid for s in j) else 1 for j in jobs], dtype=np.int32)
+    packed = PackedJobs(job_off=job_off, pk_off=pk_off, pubkeys=pubkeys, msgs=msgs.reshape(-1).copy(),
+                        sigs=sigs.reshape(-1).copy(), sig_sizes=None)
+    return Workload(name=name, packed=packed, n_invalid_jobs=int((expected == 0).sum()), expected=expected)
+
+
+def _block(rng, base_v: int, sync_k: int = 358, att_k: int = 256, n_att: int = 128) -> List[SetSpec]:
+    sets = [SetSpec([base_v], 1), SetSpec([base_v], 2)]
+    for a in range(n_att):
+        sets.append(SetSpec([int(x) for x in rng.integers(0, 1 << 20, att_k)], 3))
+    sets.append(SetSpec([int(x) for x in rng.integers(0, 1 << 20, sync_k)], 4))
+    return sets
+
+
+def c1_specs(rng):
+    return [[SetSpec([i], 0) for i in range(128)]]
+
+
+def c2_specs(rng):
+    return [_block(rng, 7)]
+
+
+def c3_specs(rng, n_att: int = 16384, n_agg: int = 1024, agg_k: int = 256):
+    jobs = [[SetSpec([int(rng.integers(0, 1 << 20))], 3)] for _ in range(n_att)]
+    for _ in range(n_agg):
+        v = int(rng.integers(0, 1 << 20))
+        jobs.append([SetSpec([v], 5), SetSpec([v], 6), SetSpec([int(x) for x in rng.integers(0, 1 << 20, agg_k)], 3)])
+    return jobs
+
+
+def c4_specs(rng, invalid_rate: float = 1e-3):
+    jobs = [[SetSpec([int(rng.integers(0, 512))], 7)] for _ in range(512)]
+    for _ in range(64):
+        v = int(rng.integers(0, 512))
+        jobs.append([SetSpec([v], 8), SetSpec([v], 9), SetSpec([int(x) for x in rng.integers(0, 512, 128)], 7)])
+    jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 7)])
+    for _ in range(4):
+        jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 10)])
+    n_sets = sum(len(j) for j in jobs)
+    n_bad = max(1, int(round(n_sets * invalid_rate)))
+    flat = [s for j in jobs for s in j]
+    for i in rng.choice(len(flat), n_bad, replace=False):
+        flat[int(i)].invalid = True
+    return jobs
+
+
+def c5_specs(rng, n_blocks: int = 32):
+    return [_block(rng, 11 + b) for b in range(n_blocks)]
+
+
+SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c4": c4_specs, "c5": c5_specs}
+
+
+def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:
+    rng = np.random.default_rng(seed)
+    return build(engine, SPECS[name](rng, **kw), name, keys=keys, seed=seed)

@@ -852,3 +852,37 @@ def deposit_message_root(pubkey48: bytes, withdrawal_credentials: bytes, amount:
 
 def compute_signing_root(object_root: bytes, domain: bytes) -> bytes:
     return _sha(object_root + domain)
+
+
+# --------------------------------------------------------------------------- job semantics
+def verify_job(sets, scalars=None):
+    """One BlsWorkReq's result as the reference computes it.
+    sets: list of (pubkeys96: list[bytes], signing_root32: bytes, signature: bytes).
+    Returns True/False or raises BlsError(name).  Error precedence follows the reference:
+      1. main thread getAggregatedPubkey (utils.ts:5-16): empty aggregate -> EMPTY_AGGREGATE_ARRAY
+      2. worker deserializeSet (worker.ts:110-116): PublicKey.fromBytes(96 B) decode errors
+      3. maybeBatch.ts:18-25 / :36: Signature.fromBytes(sig, affine, validate=true) in set order
+      4. mul_n_aggregate / core verify: infinite aggregate pubkey -> BLST_PK_IS_INFINITY
+    An infinite signature is skipped in the aggregate (blst), so such a set verifies false
+    (parity unpinned: no reference test covers it)."""
+    if len(sets) == 0:
+        raise BlsError("Empty signature set")
+    for pks, _, _ in sets:
+        if len(pks) == 0:
+            raise BlsError("EMPTY_AGGREGATE_ARRAY")
+    agg = []
+    for pks, _, _ in sets:
+        acc = None
+        for pk in pks:
+            acc = g1_add(acc, g1_deserialize(pk))
+        agg.append(acc)
+    sigs = [signature_from_bytes(s, True) for _, _, s in sets]
+    for a in agg:
+        if a is None:
+            raise BlsError("BLST_PK_IS_INFINITY")
+    if len(sets) >= 2:
+        return verify_multiple_signatures([(a, m, sg) for a, (_, m, _), sg in zip(agg, sets, sigs)], scalars)
+    a, (_, m, _), sg = agg[0], sets[0], sigs[0]
+    if sg is None:
+        return False
+    return core_verify(a, m, sg)

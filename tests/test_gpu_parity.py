@@ -1,0 +1,201 @@
+"""Parity of the HIP path (through the C ABI) with the reference semantics, on MI355X.
+Expected values come from the committed golden fixtures (oracle + reference KATs); large
+batches use size-independent properties (all-valid accepts; exactly the planted invalid
+jobs are rejected; partial products over shards agree)."""
+import asyncio
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_json
+from lodestar_amd.engine import BlsError, SetInput, pack_jobs
+
+pytestmark = pytest.mark.gpu
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def interop_sk(i):
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return int.from_bytes(d, "little") % R
+
+
+def case_jobs():
+    cases = load_json("jobs.json")["cases"]
+    jobs = []
+    for c in cases:
+        jobs.append([SetInput([bytes.fromhex(p) for p in s["pubkeys"]], bytes.fromhex(s["signing_root"]),
+                              bytes.fromhex(s["signature"])) for s in c["sets"]])
+    return cases, jobs
+
+
+def code_to_expected(code, engine):
+    if code < 0:
+        from lodestar_amd import _native as N
+        return N.error_name(-code)
+    return bool(code)
+
+
+def test_golden_jobs_one_batch(engine):
+    cases, jobs = case_jobs()
+    codes = engine.verify_jobs(jobs)
+    for c, code in zip(cases, codes):
+        assert code_to_expected(code, engine) == c["expected"], c["name"]
+
+
+def test_golden_jobs_each_alone_fixed_scalars(engine):
+    cases, jobs = case_jobs()
+    for c, job in zip(cases, jobs):
+        sc = np.arange(1, len(job) + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) | np.uint64(1)
+        code = engine.verify_jobs([job], scalars=sc if len(job) else None)[0]
+        assert code_to_expected(code, engine) == c["expected"], c["name"]
+
+
+def test_k2_k4_reference_signatures(engine):
+    k = load_json("reference_kats.json")
+    k2 = k["K2_deposit_signature"]
+    job = [SetInput([bytes.fromhex(k2["pubkey96"])], bytes.fromhex(k2["signing_root"]), bytes.fromhex(k2["signature"]))]
+    k4 = [SetInput([bytes.fromhex(s["pubkey96"])], bytes.fromhex(s["signing_root"]), bytes.fromhex(s["signature"]))
+          for s in k["K4_multithread_sets"]["sets"]]
+    assert engine.verify_jobs([job, k4, k4[:1], k4[1:]]) == [1, 1, 1, 1]
+
+
+def test_keygen_and_sign_kernels_match_kats(engine):
+    k = load_json("reference_kats.json")
+    pk48, pk96 = engine.sk_to_pk([interop_sk(i) for i in range(8)])
+    for i in range(8):
+        assert pk48[i].tobytes().hex() == k["K1_interop_pubkeys"]["pubkeys"][i]
+    k2 = k["K2_deposit_signature"]
+    sig = engine.sign([interop_sk(0)], np.frombuffer(bytes.fromhex(k2["signing_root"]), np.uint8))
+    assert sig[0].tobytes().hex() == k2["signature"]
+    for s in k["K4_multithread_sets"]["sets"]:
+        sg = engine.sign([int(s["sk"], 16)], np.frombuffer(bytes.fromhex(s["signing_root"]), np.uint8))
+        assert sg[0].tobytes().hex() == s["signature"]
+
+
+def test_aggregate_pubkeys_bytes(engine):
+    a = load_json("aggregates.json")
+    sets = [[bytes.fromhex(p) for p in g["pubkeys"]] for g in a["aggregate"]]
+    out, st = engine.aggregate_pubkeys(sets)
+    from lodestar_amd import _native as N
+    for g, o_, s in zip(a["aggregate"], out, st):
+        assert N.error_name(s) == g["status"]
+        if s == 0:
+            assert o_.hex() == g["expected96"]
+
+
+def test_g1_decompress(engine):
+    a = load_json("aggregates.json")["g1_decompress"]
+    out, st = engine.g1_decompress([bytes.fromhex(x["in48"]) for x in a], validate=True)
+    assert st == [0] * len(a)
+    assert [o_.hex() for o_ in out] == [x["out96"] for x in a]
+    bad = bytes([0xC0]) + bytes(47)
+    _, st = engine.g1_decompress([bad], validate=True)
+    assert st == [6]  # BLST_PK_IS_INFINITY
+
+
+def make_batch(engine, n_sets, agg_k=1, seed=1, invalid=()):
+    """n_sets single-job sets (k pubkeys each over a 64-key pool) signed on the GPU."""
+    rng = np.random.default_rng(seed)
+    pool = [interop_sk(i) for i in range(64)]
+    _, pk96 = engine.sk_to_pk(pool)
+    msgs = rng.integers(0, 256, size=(n_sets, 32), dtype=np.uint8)
+    idx = rng.integers(0, 64, size=(n_sets, agg_k))
+    sks = [sum(pool[j] for j in row) % R for row in idx]
+    sigs = engine.sign(sks, msgs)
+    jobs = []
+    for i in range(n_sets):
+        m = msgs[i].tobytes()
+        if i in invalid:
+            m = bytes([m[0] ^ 1]) + m[1:]
+        jobs.append([SetInput([pk96[j].tobytes() for j in idx[i]], m, sigs[i].tobytes())])
+    return jobs
+
+
+def test_bisection_finds_planted_invalid_jobs(engine):
+    bad = {3, 77, 200, 201, 511}
+    jobs = make_batch(engine, 512, agg_k=1, seed=7, invalid=bad)
+    codes = engine.verify_jobs(jobs)
+    assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
+    assert all(codes[i] == 0 for i in bad)
+
+
+def test_aggregate_sets_and_multi_set_jobs(engine):
+    jobs = make_batch(engine, 96, agg_k=33, seed=3)
+    merged = [sum(jobs[i:i + 8], []) for i in range(0, 96, 8)]
+    assert engine.verify_jobs(merged) == [1] * 12
+    bad = make_batch(engine, 96, agg_k=33, seed=3, invalid={50})
+    merged = [sum(bad[i:i + 8], []) for i in range(0, 96, 8)]
+    assert engine.verify_jobs(merged) == [1] * 6 + [0] + [1] * 5
+
+
+def test_partials_over_shards(engine):
+    jobs = make_batch(engine, 200, seed=11)
+    parts = []
+    for sh in (jobs[:70], jobs[70:140], jobs[140:]):
+        b = engine.upload(sh)
+        f, st = b.partial()
+        assert list(st) == [1] * len(sh)
+        parts.append(f)
+        b.free()
+    assert engine.product_is_one(parts)
+    bad = make_batch(engine, 70, seed=11, invalid={5})
+    b = engine.upload(bad)
+    fbad, _ = b.partial()
+    b.free()
+    assert not engine.product_is_one([fbad] + parts[1:])
+
+
+def test_random_scalars_repeatable_verdicts(engine):
+    jobs = make_batch(engine, 64, seed=5, invalid={9})
+    b = engine.upload(jobs)
+    for _ in range(3):
+        codes = list(b.verify())
+        assert codes == [1] * 9 + [0] + [1] * 54
+    b.free()
+
+
+def test_pool_multithread_e2e_cases(engine):
+    """packages/beacon-node/test/e2e/chain/bls/multithread.test.ts:60-103 on the GPU pool."""
+    from lodestar_amd import verifier as V
+    k4 = load_json("reference_kats.json")["K4_multithread_sets"]["sets"]
+    sets = [V.SingleSignatureSet(V.PublicKey(bytes.fromhex(s["pubkey96"])), bytes.fromhex(s["signing_root"]),
+                                 bytes.fromhex(s["signature"])) for s in k4]
+
+    async def many(sleep, opts):
+        pool = V.BlsGpuVerifier(engine=engine)
+        futs = []
+        for _ in range(8):
+            futs.append(asyncio.ensure_future(pool.verify_signature_sets(sets, opts)))
+            if sleep:
+                await asyncio.sleep(0.005)
+        res = await asyncio.gather(*futs)
+        await pool.close()
+        return res
+
+    assert asyncio.run(many(False, None)) == [True] * 8
+    assert asyncio.run(many(True, None)) == [True] * 8
+    assert asyncio.run(many(True, V.VerifySignatureOpts(batchable=True))) == [True] * 8
+
+    async def first_invalid():
+        pool = V.BlsGpuVerifier(engine=engine)
+        inv = V.SingleSignatureSet(sets[0].pubkey, sets[0].signing_root, bytes(32))
+        bad = asyncio.ensure_future(pool.verify_signature_sets([inv], V.VerifySignatureOpts(batchable=True)))
+        goods = [asyncio.ensure_future(pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True)))
+                 for _ in range(8)]
+        with pytest.raises(BlsError, match="BLST_INVALID_SIZE"):
+            await bad
+        res = await asyncio.gather(*goods)
+        await pool.close()
+        return res
+
+    assert asyncio.run(first_invalid()) == [True] * 8
+
+    async def main_thread():
+        pool = V.BlsGpuVerifier(engine=engine)
+        r = await pool.verify_signature_sets(sets, V.VerifySignatureOpts(verify_on_main_thread=True))
+        await pool.close()
+        return r
+
+    assert asyncio.run(main_thread()) is True
