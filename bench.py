@@ -45,6 +45,49 @@ def load_counts():
         return json.load(f)
 
 
+def stage_work(counts, packed):
+    """Algorithmic Fp multiplications per pipeline stage for this batch (profiles/roofline_counts.json
+    from tools/count_ops.py: per-item counts of exactly the arithmetic each kernel runs)."""
+    c = counts["fp_mul_per_item"]
+    n = packed.n_sets
+    k = np.diff(packed.pk_off.astype(np.int64))
+    sets_per_job = np.diff(packed.job_off.astype(np.int64))
+    m = 1
+    while m < packed.n_jobs:
+        m *= 2
+    blind = np.where(k == 1, c["pk_blind_k1"], c["pk_blind_k_base"] + c["pk_blind_per_extra_key"] * k).sum()
+    return {
+        "decode_sigs": n * c["decode_sigs"],
+        "hash_map": 2 * n * c["hash_map"],
+        "hash_finish": n * c["hash_finish"],
+        "pk_blind": float(blind),
+        "miller": n * c["miller"],
+        "job_leaves": float(((sets_per_job - 1).clip(0) * c["fp12_mul"] + sets_per_job * c["g2_add"]).sum()),
+        "tree_up": (m - 1) * (c["fp12_mul"] + c["g2_add"]),
+        "root_check": c["node_check"],
+    }
+
+
+def roofline(counts, packed, stage_ms):
+    if not counts or not stage_ms:
+        return None
+    work = stage_work(counts, packed)
+    mac = counts["mac_per_fp_mul"]
+    peak = counts["peak_tmac_s"]
+    per = {}
+    for k, fm in work.items():
+        if stage_ms.get(k, 0) > 0:
+            t = stage_ms[k] * 1e-3
+            per[k] = {"ms": round(stage_ms[k], 3), "fp_mul": int(fm), "tmac_s": round(fm * mac / t / 1e12, 3),
+                      "frac": round(fm * mac / t / 1e12 / peak, 4)}
+    dom = max(per, key=lambda k: per[k]["ms"])
+    ach = per[dom]["tmac_s"]
+    return {"bound": "valu-int", "kernel": "k_" + dom, "achieved": ach, "peak": peak,
+            "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": None,
+            "whole_pipeline_frac": round(sum(work.values()) * mac / (sum(stage_ms.values()) * 1e-3) / 1e12 / peak, 4),
+            "stages": per}
+
+
 def main():
     a = parse()
     import torch
@@ -107,21 +150,7 @@ def main():
     value = n_sets * world * a.steps / el
     stage_ms = {k: v / a.steps for k, v in stage_ms.items()}
 
-    roof = None
-    counts = load_counts()
-    if counts:
-        dom = max((k for k in stage_ms if k in counts["per_launch_mul"]), key=lambda k: stage_ms[k], default=None)
-        if dom:
-            muls = counts["per_launch_mul"][dom](n_sets) if callable(counts["per_launch_mul"][dom]) else None
-            per_item = counts["per_item_mul"][dom]
-            items = n_sets * counts["items_per_set"].get(dom, 1)
-            mul_total = per_item * items
-            ach = mul_total / (stage_ms[dom] * 1e-3) / 1e12
-            peak = counts["peak_tmul_s"]
-            roof = {"bound": "valu-int", "kernel": "k_" + dom, "achieved": round(ach, 4), "peak": peak,
-                    "unit": "T int32-mul/s", "frac": round(ach / peak, 4), "traffic": counts.get("traffic", {}).get(dom),
-                    "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()}}
-
+    roof = roofline(load_counts(), wl.packed, stage_ms)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:

@@ -20,6 +20,15 @@
 
 #define LB_UNROLL _Pragma("unroll")
 
+// Host-only operation counter (tools/count_ops.py builds the harness with -DLB_COUNT_OPS to
+// derive the algorithmic Fp-multiplication count per pipeline stage for the roofline).
+#if defined(LB_COUNT_OPS) && !defined(__HIPCC__)
+extern unsigned long long lb_count_mul;
+#define LB_COUNT_MUL() (lb_count_mul++)
+#else
+#define LB_COUNT_MUL() ((void)0)
+#endif
+
 // Status codes (blst BLST_ERROR values + Lodestar's own errors) are the public ones of
 // the C ABI: include/lodestar_bls.h.  Per-set / per-job status uses them directly.
 #include "lodestar_bls.h"

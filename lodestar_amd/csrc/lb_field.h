@@ -112,6 +112,7 @@ LB_HD fp fp_dbl(const fp& a) { return fp_add(a, a); }
 // pipeline kernels inside the instruction cache (a fully inlined Miller loop is >1 MB of
 // code) and keeps compile time bounded.  Arguments travel in VGPRs (2 x 12 words).
 LB_NI fp fp_mul(fp a, fp b) {
+  LB_COUNT_MUL();
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
   uint32_t t[14];
   LB_UNROLL for (int j = 0; j < 14; j++) t[j] = 0;
