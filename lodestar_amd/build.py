@@ -70,7 +70,7 @@ def build_cpu_pool(force=False, verbose=True):
     os.makedirs(os.path.dirname(CPU_POOL), exist_ok=True)
     if not force and not _stale(CPU_POOL, _deps() + [src]):
         return CPU_POOL
-    cmd = ["g++", "-O3", "-march=x86-64-v3", "-shared", "-fPIC", "-pthread", "-I" + INC, "-I" + CSRC, src,
+    cmd = ["g++", "-O3", "-shared", "-fPIC", "-pthread", "-I" + INC, "-I" + CSRC, src,
            "-o", CPU_POOL + ".tmp"]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
