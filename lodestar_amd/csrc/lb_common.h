@@ -8,8 +8,8 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define LB_HD __host__ __device__ __forceinline__
-#define LB_HDNI __host__ __device__ __attribute__((noinline))
-#define LB_NI __host__ __device__ __attribute__((noinline))
+#define LB_HDNI static __host__ __device__ __attribute__((noinline))
+#define LB_NI static __host__ __device__ __attribute__((noinline))
 #define LB_CONST static __constant__ const
 #else
 #define LB_HD static inline

@@ -107,36 +107,95 @@ LB_HD fp fp_sub(const fp& a, const fp& b) {
 LB_HD fp fp_neg(const fp& a) { return fp_sub(fp_zero(), a); }
 LB_HD fp fp_dbl(const fp& a) { return fp_add(a, a); }
 
-// Montgomery multiplication, CIOS with 32-bit limbs: a*b/R mod p.
-// Not inlined on the GPU: one ~450-instruction body shared by every call site keeps the
-// pipeline kernels inside the instruction cache (a fully inlined Miller loop is >1 MB of
-// code) and keeps compile time bounded.  Arguments travel in VGPRs (2 x 12 words).
-LB_NI fp fp_mul(fp a, fp b) {
-  LB_COUNT_MUL();
+// Montgomery multiplication a*b/R mod p, 12 x 32-bit limbs, operand scanning in carry-save
+// form.  Textbook CIOS threads one carry through all 288 multiply-adds, so a lone wave waits
+// on a 288-deep v_mad_u64_u32 dependency chain.  Here every row keeps the carry out of limb j
+// *pending* for limb j+1 of the next row: u = a_i*b_j + t_j + cc_j <= (2^32-1)^2 + 2(2^32-1)
+// < 2^64, so each row's 12 products are independent and the chain is ~7 deep per row.
+// After the multiply row nothing is pending into limb 0, so m = t_0 * (-p^-1) mod 2^32 is
+// exact; the reduction row zeroes limb 0 and the state shifts down one limb.
+LB_HD fp fp_mul_body(const fp& a, const fp& b) {
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
-  uint32_t t[14];
-  LB_UNROLL for (int j = 0; j < 14; j++) t[j] = 0;
+  uint32_t t[13], cc[14];
+  LB_UNROLL for (int j = 0; j < 13; j++) t[j] = 0;
+  LB_UNROLL for (int j = 0; j < 14; j++) cc[j] = 0;
   LB_UNROLL for (int i = 0; i < 12; i++) {
-    uint64_t c = 0;
+    uint32_t n[14];
+    n[0] = 0;
     LB_UNROLL for (int j = 0; j < 12; j++) {
-      c = (uint64_t)a.v[i] * b.v[j] + t[j] + (c >> 32);
-      t[j] = (uint32_t)c;
+      uint64_t u = (uint64_t)a.v[i] * b.v[j] + t[j] + cc[j];
+      t[j] = (uint32_t)u;
+      n[j + 1] = (uint32_t)(u >> 32);
     }
-    c = (uint64_t)t[12] + (c >> 32);
-    t[12] = (uint32_t)c;
-    t[13] = (uint32_t)(c >> 32);
+    {
+      uint64_t u = (uint64_t)t[12] + cc[12];
+      t[12] = (uint32_t)u;
+      n[13] = (uint32_t)(u >> 32) + cc[13];
+    }
+    // reduction row: limb 0 has no pending carry now
     uint32_t m = t[0] * LB_PINV;
-    c = (uint64_t)m * Pl[0] + t[0];
-    LB_UNROLL for (int j = 1; j < 12; j++) {
-      c = (uint64_t)m * Pl[j] + t[j] + (c >> 32);
-      t[j - 1] = (uint32_t)c;
+    uint32_t r[14];
+    r[0] = 0;
+    LB_UNROLL for (int j = 0; j < 12; j++) {
+      uint64_t u = (uint64_t)m * Pl[j] + t[j] + n[j];
+      t[j] = (uint32_t)u;
+      r[j + 1] = (uint32_t)(u >> 32);
     }
-    c = (uint64_t)t[12] + (c >> 32);
-    t[11] = (uint32_t)c;
-    t[12] = t[13] + (uint32_t)(c >> 32);
+    {
+      uint64_t u = (uint64_t)t[12] + n[12];
+      t[12] = (uint32_t)u;
+      r[13] = (uint32_t)(u >> 32) + n[13];
+    }
+    // divide by 2^32: limb 0 is zero; pending carries shift with the limbs
+    LB_UNROLL for (int j = 0; j < 12; j++) t[j] = t[j + 1];
+    t[12] = 0;
+    LB_UNROLL for (int j = 0; j < 13; j++) cc[j] = r[j + 1];
+    cc[13] = 0;
   }
-  return fp_reduce_once(t, t[12]);
+  // resolve the pending carries (value < 2p < 2^382, so nothing escapes limb 12)
+  uint32_t o[12];
+  uint64_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    c = (uint64_t)t[j] + cc[j] + (c >> 32);
+    o[j] = (uint32_t)c;
+  }
+  uint32_t top = t[12] + cc[12] + (uint32_t)(c >> 32);
+  return fp_reduce_once(o, top);
 }
+
+#if defined(__HIPCC__)
+// Out of line on the GPU: one body shared by every call site keeps the pipeline kernels inside
+// the instruction cache and compile time bounded.  Operands and result travel as 16-wide
+// vectors, which the AMDGPU calling convention keeps in VGPRs (a 48-byte struct would be
+// passed through scratch memory).
+typedef uint32_t lb_v16u __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ lb_v16u fp_pack(const fp& a) {
+  lb_v16u r;
+  LB_UNROLL for (int i = 0; i < 12; i++) r[i] = a.v[i];
+  r[12] = r[13] = r[14] = r[15] = 0;
+  return r;
+}
+__device__ __forceinline__ fp fp_unpack(lb_v16u a) {
+  fp r;
+  LB_UNROLL for (int i = 0; i < 12; i++) r.v[i] = a[i];
+  return r;
+}
+static __device__ __attribute__((noinline)) lb_v16u fp_mul_v(lb_v16u a, lb_v16u b) {
+  return fp_pack(fp_mul_body(fp_unpack(a), fp_unpack(b)));
+}
+__host__ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fp_unpack(fp_mul_v(fp_pack(a), fp_pack(b)));
+#else
+  return fp_mul_body(a, b);
+#endif
+}
+#else
+static inline fp fp_mul(const fp& a, const fp& b) {
+  LB_COUNT_MUL();
+  return fp_mul_body(a, b);
+}
+#endif
 
 LB_HD fp fp_sqr(const fp& a) { return fp_mul(a, a); }
 
@@ -225,30 +284,18 @@ LB_HD fp2 fp2_mul3(const fp2& a) { return fp2{fp_mul3(a.c0), fp_mul3(a.c1)}; }
 LB_HD fp2 fp2_mul4(const fp2& a) { return fp2{fp_mul4(a.c0), fp_mul4(a.c1)}; }
 LB_HD fp2 fp2_mul8(const fp2& a) { return fp2{fp_mul8(a.c0), fp_mul8(a.c1)}; }
 
-// Tower layers above Fp are out-of-line with pointer arguments (values live in the
-// caller's frame); only fp_mul's operands travel in registers.
-LB_NI void fp2_mul_p(fp2* r, const fp2* pa, const fp2* pb) {
-  fp2 a = *pa, b = *pb;
+// Fp2 arithmetic is inline (its three products are calls to fp_mul); the Fp6 / Fp12 layers
+// and the group law are out of line with pointer / by-value arguments.
+LB_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
   fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  *r = fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-LB_NI void fp2_sqr_p(fp2* r, const fp2* pa) {
-  fp2 a = *pa;
-  fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  fp t1 = fp_mul(a.c0, a.c1);
-  *r = fp2{t0, fp_dbl(t1)};
-}
-LB_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
-  fp2 r;
-  fp2_mul_p(&r, &a, &b);
-  return r;
+  return fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 LB_HD fp2 fp2_sqr(const fp2& a) {
-  fp2 r;
-  fp2_sqr_p(&r, &a);
-  return r;
+  fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp t1 = fp_mul(a.c0, a.c1);
+  return fp2{t0, fp_dbl(t1)};
 }
 // multiply by the non-residue xi = 1 + u
 LB_HD fp2 fp2_mul_xi(const fp2& a) { return fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
