@@ -20,6 +20,27 @@
 
 #define LB_UNROLL _Pragma("unroll")
 
+// 32-bit add / subtract with carry.  On the GPU these lower to one v_add_co_u32 /
+// v_addc_co_u32 (v_sub_co / v_subb_co) per limb; the uint64_t idiom costs ~6 instructions per
+// limb (zero-extension moves + 64-bit adds).  g++ builds (CPU harness) use the portable form.
+#if defined(__clang__)
+#define LB_ADDC(a, b, cin, cout) __builtin_addc((a), (b), (cin), (cout))
+#define LB_SUBC(a, b, bin, bout) __builtin_subc((a), (b), (bin), (bout))
+#else
+static inline uint32_t lb_addc_port(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+static inline uint32_t lb_subc_port(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+#define LB_ADDC(a, b, cin, cout) lb_addc_port((a), (b), (cin), (cout))
+#define LB_SUBC(a, b, bin, bout) lb_subc_port((a), (b), (bin), (bout))
+#endif
+
 // Host-only operation counter (tools/count_ops.py builds the harness with -DLB_COUNT_OPS to
 // derive the algorithmic Fp-multiplication count per pipeline stage for the roofline).
 #if defined(LB_COUNT_OPS) && !defined(__HIPCC__)

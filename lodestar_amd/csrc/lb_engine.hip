@@ -303,7 +303,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                      e->job_status.as<int32_t>());
   mark(6);
   for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
-    hipLaunchKernelGGL(k_tree_up, dim3(nblk(lo)), dim3(LB_TPB), 0, s, m, lo, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL(k_tree_up, dim3(lo + nblk(lo)), dim3(64), 0, s, m, lo, e->treeP.as<uint32_t>(),
                        e->treeS.as<uint32_t>());
   mark(7);
   LB_HIP(hipGetLastError());
@@ -317,7 +317,7 @@ static int32_t check_nodes(lb_engine* e, uint32_t m, const std::vector<uint32_t>
   LB_HIP(e->nodes.ensure((size_t)c * 4));
   LB_HIP(e->verdict.ensure((size_t)c * 4));
   LB_HIP(hipMemcpyAsync(e->nodes.p, nodes.data(), (size_t)c * 4, hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_node_check, dim3(nblk(c)), dim3(LB_TPB), 0, e->stream, m, c, e->nodes.as<uint32_t>(),
+  hipLaunchKernelGGL(k_node_check, dim3(c), dim3(64), 0, e->stream, m, c, e->nodes.as<uint32_t>(),
                      e->treeP.as<uint32_t>(), e->treeS.as<uint32_t>(), e->verdict.as<int32_t>());
   LB_HIP(hipGetLastError());
   LB_HIP(hipMemcpyAsync(v.data(), e->verdict.p, (size_t)c * 4, hipMemcpyDeviceToHost, e->stream));
@@ -421,7 +421,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   int32_t st = run_pipeline(e, b, scalars, m);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
-  hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(LB_TPB), 0, e->stream, m, e->treeP.as<uint32_t>(),
+  hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
                      e->treeS.as<uint32_t>(), e->parts.as<uint8_t>());
   LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(b->n_jobs);
@@ -444,7 +444,7 @@ extern "C" int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials5
   LB_HIP(e->parts.ensure((size_t)(n ? n : 1) * 576));
   LB_HIP(e->ok.ensure(4));
   if (n) LB_HIP(hipMemcpyAsync(e->parts.p, partials576, (size_t)n * 576, hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(LB_TPB), 0, e->stream, n, e->parts.as<uint8_t>(),
+  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(64), 0, e->stream, n, e->parts.as<uint8_t>(),
                      e->ok.as<int32_t>());
   LB_HIP(hipGetLastError());
   LB_HIP(hipMemcpyAsync(ok, e->ok.p, 4, hipMemcpyDeviceToHost, e->stream));

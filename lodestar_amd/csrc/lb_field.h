@@ -63,11 +63,7 @@ LB_HD fp fp_reduce_once(const uint32_t* t, uint32_t top) {
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
   uint32_t s[12];
   uint32_t br = 0;
-  LB_UNROLL for (int j = 0; j < 12; j++) {
-    uint64_t d = (uint64_t)t[j] - Pl[j] - br;
-    s[j] = (uint32_t)d;
-    br = (uint32_t)(d >> 63);
-  }
+  LB_UNROLL for (int j = 0; j < 12; j++) s[j] = LB_SUBC(t[j], Pl[j], br, &br);
   bool ge = (top != 0) || (br == 0);
   fp r;
   LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = ge ? s[j] : t[j];
@@ -76,31 +72,21 @@ LB_HD fp fp_reduce_once(const uint32_t* t, uint32_t top) {
 
 LB_HD fp fp_add(const fp& a, const fp& b) {
   uint32_t t[12];
-  uint64_t c = 0;
-  LB_UNROLL for (int j = 0; j < 12; j++) {
-    c = (uint64_t)a.v[j] + b.v[j] + (c >> 32);
-    t[j] = (uint32_t)c;
-  }
-  return fp_reduce_once(t, (uint32_t)(c >> 32));
+  uint32_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) t[j] = LB_ADDC(a.v[j], b.v[j], c, &c);
+  return fp_reduce_once(t, c);
 }
 
 LB_HD fp fp_sub(const fp& a, const fp& b) {
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
   uint32_t t[12];
   uint32_t br = 0;
-  LB_UNROLL for (int j = 0; j < 12; j++) {
-    uint64_t d = (uint64_t)a.v[j] - b.v[j] - br;
-    t[j] = (uint32_t)d;
-    br = (uint32_t)(d >> 63);
-  }
+  LB_UNROLL for (int j = 0; j < 12; j++) t[j] = LB_SUBC(a.v[j], b.v[j], br, &br);
   // if borrow, add p back
   uint32_t m = 0u - br;
   fp r;
-  uint64_t c = 0;
-  LB_UNROLL for (int j = 0; j < 12; j++) {
-    c = (uint64_t)t[j] + (Pl[j] & m) + (c >> 32);
-    r.v[j] = (uint32_t)c;
-  }
+  uint32_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = LB_ADDC(t[j], Pl[j] & m, c, &c);
   return r;
 }
 
@@ -154,12 +140,9 @@ LB_HD fp fp_mul_body(const fp& a, const fp& b) {
   }
   // resolve the pending carries (value < 2p < 2^382, so nothing escapes limb 12)
   uint32_t o[12];
-  uint64_t c = 0;
-  LB_UNROLL for (int j = 0; j < 12; j++) {
-    c = (uint64_t)t[j] + cc[j] + (c >> 32);
-    o[j] = (uint32_t)c;
-  }
-  uint32_t top = t[12] + cc[12] + (uint32_t)(c >> 32);
+  uint32_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) o[j] = LB_ADDC(t[j], cc[j], c, &c);
+  uint32_t top = t[12] + cc[12] + c;
   return fp_reduce_once(o, top);
 }
 
@@ -222,7 +205,98 @@ LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) {
   return r;
 }
 
-LB_HD fp fp_inv(const fp& a) { return fp_pow_const(a, LB_EXP_PM2, 380); }          // a^(p-2); inv(0)=0
+// ---- variable-time inversion (binary extended Euclid).  Every value this engine inverts is
+// derived from public data (signatures, pubkeys, messages), so timing does not leak secrets;
+// this replaces a 570-multiplication Fermat chain by ~400 cheap shift/subtract steps.
+LB_HD bool lb_is_one_plain(const uint32_t* x) {
+  uint32_t t = x[0] ^ 1u;
+  LB_UNROLL for (int i = 1; i < 12; i++) t |= x[i];
+  return t == 0;
+}
+LB_HD int lb_ctz32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_ctz(x);
+#else
+  return __builtin_ctz(x);
+#endif
+}
+// x <- x / 2^k mod p for 1 <= k <= 31 (Montgomery-style: add m*p so the low k bits vanish)
+LB_HD void lb_div2k_mod(uint32_t* x, int k) {
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t m = (x[0] * LB_PINV) & ((1u << k) - 1u);
+  uint32_t t[13];
+  uint64_t c = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    c = (uint64_t)m * Pl[j] + x[j] + (c >> 32);
+    t[j] = (uint32_t)c;
+  }
+  t[12] = (uint32_t)(c >> 32);
+  // (x + m p) < 2^k p, divisible by 2^k, result < p
+  LB_UNROLL for (int j = 0; j < 12; j++) x[j] = (t[j] >> k) | (t[j + 1] << (32 - k));
+}
+// u <- u / 2^k (plain shift), 1 <= k <= 31
+LB_HD void lb_shr(uint32_t* u, int k) {
+  LB_UNROLL for (int j = 0; j < 11; j++) u[j] = (u[j] >> k) | (u[j + 1] << (32 - k));
+  u[11] >>= k;
+}
+LB_HD bool lb_geq(const uint32_t* a, const uint32_t* b) {
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) (void)LB_SUBC(a[j], b[j], br, &br);
+  return br == 0;
+}
+LB_HD void lb_sub_in(uint32_t* a, const uint32_t* b) {
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) a[j] = LB_SUBC(a[j], b[j], br, &br);
+}
+// plain a in [0, p) -> a^-1 mod p (plain), 0 -> 0
+LB_NI fp fp_inv_plain_vt(fp a) {
+  if (fp_is_zero(a)) return a;
+  uint32_t u[12], v[12];
+  fp x1 = fp_zero(), x2 = fp_zero();
+  x1.v[0] = 1;
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    u[j] = a.v[j];
+    v[j] = Pl[j];
+  }
+  // invariant: x1 * a == u, x2 * a == v (mod p); u, v > 0, v odd at loop head
+  while (true) {
+    while (u[0] == 0) {  // rare: shift whole words
+      LB_UNROLL for (int j = 0; j < 11; j++) u[j] = u[j + 1];
+      u[11] = 0;
+      lb_div2k_mod(x1.v, 16);
+      lb_div2k_mod(x1.v, 16);
+    }
+    int k = lb_ctz32(u[0]);
+    if (k) {
+      lb_shr(u, k);
+      lb_div2k_mod(x1.v, k);
+    }
+    if (lb_is_one_plain(u)) return x1;
+    if (lb_geq(u, v)) {
+      lb_sub_in(u, v);
+      x1 = fp_sub(x1, x2);
+    } else {
+      lb_sub_in(v, u);
+      x2 = fp_sub(x2, x1);
+      // v - u is even (both odd): normalise v here
+      while (v[0] == 0) {
+        LB_UNROLL for (int j = 0; j < 11; j++) v[j] = v[j + 1];
+        v[11] = 0;
+        lb_div2k_mod(x2.v, 16);
+        lb_div2k_mod(x2.v, 16);
+      }
+      int kv = lb_ctz32(v[0]);
+      if (kv) {
+        lb_shr(v, kv);
+        lb_div2k_mod(x2.v, kv);
+      }
+      if (lb_is_one_plain(v)) return x2;
+    }
+  }
+}
+// Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
+LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
 LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
 LB_HD bool fp_is_square(const fp& a) {
   // Legendre symbol a^((p-1)/2) in {0, 1, -1}

@@ -55,6 +55,8 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 
 __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
+#include "lb_wave.h"
+
 // ---------------------------------------------------------------- signatures
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
 __global__ void __launch_bounds__(LB_TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
@@ -218,58 +220,69 @@ __global__ void __launch_bounds__(LB_TPB) k_job_leaves(uint32_t n_jobs, uint32_t
   soa_st(treeS, 2 * m, m + j, S);
 }
 
-// nodes [lo, 2 lo): node i = node 2i (x) node 2i+1
-__global__ void __launch_bounds__(LB_TPB) k_tree_up(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP,
-                                                    uint32_t* __restrict__ treeS) {
-  uint32_t t = lb_tid();
-  if (t >= lo) return;
-  uint32_t i = lo + t;
-  fp12 a = soa_ld<fp12>(treeP, 2 * m, 2 * i), b = soa_ld<fp12>(treeP, 2 * m, 2 * i + 1);
-  soa_st(treeP, 2 * m, i, fp12_mul(a, b));
-  g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
-  soa_st(treeS, 2 * m, i, s);
+// Product tree over jobs, one level: nodes [lo, 2 lo), node i = node 2i (x) node 2i+1.
+// Blocks [0, lo): one wave per node multiplies the Fp12 children cooperatively (MUL12 program).
+// Blocks [lo, lo + ceil(lo/64)): one lane per node adds the G2 children (Jacobian).
+__global__ void __launch_bounds__(64) k_tree_up(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP,
+                                                uint32_t* __restrict__ treeS) {
+  __shared__ fp S[LBW_SLOTS];
+  if (blockIdx.x < lo) {
+    uint32_t i = lo + blockIdx.x;
+    w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
+    w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
+    w_mul(S, LBW_A(2), LBW_A(0), LBW_A(1));
+    w_store_soa12(S, LBW_A(2), treeP, 2 * m, i);
+  } else {
+    uint32_t t = (blockIdx.x - lo) * 64 + threadIdx.x;
+    if (t >= lo) return;
+    uint32_t i = lo + t;
+    g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
+    soa_st(treeS, 2 * m, i, s);
+  }
 }
 
-// f = P * ML(-G1, S)
-__device__ __forceinline__ fp12 node_partial(const fp12& P, const g2j& S) {
-  if (jac_is_inf(S)) return P;
-  g2a sa;
-  jac_to_aff(sa, S);
-  g1a ng1{fp_load(LB_G1X), fp_load(LB_G1NEGY)};
-  return fp12_mul(P, miller_loop(ng1, sa));
-}
-
-__global__ void __launch_bounds__(LB_TPB) k_node_check(uint32_t m, uint32_t cnt, const uint32_t* __restrict__ nodes,
-                                                       const uint32_t* __restrict__ treeP,
-                                                       const uint32_t* __restrict__ treeS,
-                                                       int32_t* __restrict__ verdict) {
-  uint32_t t = lb_tid();
-  if (t >= cnt) return;
-  uint32_t i = nodes[t];
-  fp12 f = node_partial(soa_ld<fp12>(treeP, 2 * m, i), soa_ld<g2j>(treeS, 2 * m, i));
-  verdict[t] = fp12_is_one(final_exponentiation(f)) ? 1 : 0;
+// One wave per checked node: verdict = FE(P * ML(-G1, S)) == 1   (Pairing.finalverify)
+__global__ void __launch_bounds__(64) k_node_check(uint32_t m, uint32_t cnt, const uint32_t* __restrict__ nodes,
+                                                   const uint32_t* __restrict__ treeP,
+                                                   const uint32_t* __restrict__ treeS, int32_t* __restrict__ verdict) {
+  __shared__ fp S[LBW_SLOTS];
+  if (blockIdx.x >= cnt) return;
+  w_init_consts(S);
+  w_node_partial(S, LBW_A(0), treeP, treeS, 2 * m, nodes[blockIdx.x]);
+  w_final_exp(S, LBW_A(0), LBW_A(0));
+  bool one = w_is_one(S, LBW_A(0));
+  if (threadIdx.x == 0) verdict[blockIdx.x] = one ? 1 : 0;
 }
 
 // root partial product as 576 bytes (multi-GPU exchange format)
-__global__ void __launch_bounds__(LB_TPB) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
-                                                         const uint32_t* __restrict__ treeS,
-                                                         uint8_t* __restrict__ out576) {
-  if (lb_tid() != 0) return;
-  fp12 f = node_partial(soa_ld<fp12>(treeP, 2 * m, 1), soa_ld<g2j>(treeS, 2 * m, 1));
-  fp12_to_be576(out576, f);
+__global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                     const uint32_t* __restrict__ treeS, uint8_t* __restrict__ out576) {
+  __shared__ fp S[LBW_SLOTS];
+  w_init_consts(S);
+  w_node_partial(S, LBW_A(0), treeP, treeS, 2 * m, 1);
+  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(S[LBW_A(0) + threadIdx.x]));
 }
 
-__global__ void __launch_bounds__(LB_TPB) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
-                                                           int32_t* __restrict__ ok) {
-  if (lb_tid() != 0) return;
-  fp12 acc = fp12_one();
-  bool good = true;
+__global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
+                                                       int32_t* __restrict__ ok) {
+  __shared__ fp S[LBW_SLOTS];
+  __shared__ int bad;
+  const int lane = threadIdx.x;
+  if (lane == 0) bad = 0;
+  w_init_consts(S);
+  w_set_one(S, LBW_A(0));
   for (uint32_t i = 0; i < n; i++) {
-    fp12 f;
-    good &= fp12_from_be576(f, parts + (size_t)576 * i);
-    acc = fp12_mul(acc, f);
+    if (lane < 12) {
+      fp x;
+      if (!fp_plain_from_be48(x, parts + (size_t)576 * i + 48 * lane, 0xff)) atomicOr(&bad, 1);
+      S[LBW_A(7) + lane] = fp_to_mont(x);
+    }
+    w_sync();
+    w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   }
-  *ok = (good && fp12_is_one(final_exponentiation(acc))) ? 1 : 0;
+  w_final_exp(S, LBW_A(0), LBW_A(0));
+  bool one = w_is_one(S, LBW_A(0));
+  if (lane == 0) *ok = (one && !bad) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- pubkey aggregation only

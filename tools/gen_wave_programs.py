@@ -1,0 +1,496 @@
+#!/usr/bin/env python3
+"""Compiles the Fp12 / Miller-step tower code into wave-cooperative programs.
+
+Output: lodestar_amd/csrc/lb_wave_progs.h (generated; do not edit).
+
+Why: a single GPU lane runs one Fp multiplication in ~2.4 us (issue-bound), so a
+final exponentiation done by one thread (~14.6k Fp mults) costs ~60-90 ms.  Here the tower
+formulas of lb_field.h / lb_pairing.h are traced symbolically: every Fp multiplication
+becomes a *product task* whose two operands are small +-integer linear combinations of
+LDS-resident Fp slots, and every value that feeds a later product (or is an output) is
+materialised by a *linear task*.  Products are scheduled at the earliest stage their
+operands allow, so one wave (64 lanes) runs e.g. all 54 products of an Fp12 multiplication
+at once.  The same Karatsuba formulas are used as in the single-thread code, so the product
+count is unchanged; only the schedule differs.
+
+Slot map (per wave, in units of one Fp element = 12 u32):
+  [0, 32)   IN     program inputs (the caller copies operands here)
+  [32, 64)  CONST  b' * 3 (2), 1/2 (1), Frobenius constants (10 + 5)
+  [64, ...) TEMP   products and materialised values; program outputs live here
+
+Encoding (int16): header [n_phases, n_temps, n_out, out_slot * n_out] padded to 8 entries,
+then per phase [kind, n_tasks, 0 x 6] + fixed-size records (PREC / LREC entries, 16-byte
+multiples, so a lane fetches its record with 16-byte vector loads); kind 0 = product phase,
+record [dst, (slot, coef) * MAXT for x, (slot, coef) * MAXT for y]; kind 1 = linear phase,
+record [dst, (slot, coef) * MAXL].  Terms are packed first; unused pairs have coef 0.
+
+The program encoding is validated here by a Python interpreter against direct big-integer
+evaluation of the same tower formulas (and, through the engine tests, against the oracle).
+"""
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+MAXT = 8
+MAXL = 24
+PREC = 40   # product record: dst + 2 x 8 (slot, coef) pairs, padded to 16-byte multiple
+LREC = 56   # linear record: dst + 24 (slot, coef) pairs, padded
+IN_BASE, CONST_BASE, TEMP_BASE = 0, 32, 64
+C_B3, C_INV2, C_FROB1, C_FROB2 = 0, 2, 3, 13   # offsets in CONST
+N_CONST = 18
+
+
+class Lin:
+    __slots__ = ("d",)
+
+    def __init__(self, d=None):
+        self.d = {k: v for k, v in (d or {}).items() if v}
+
+    def __add__(self, o):
+        d = dict(self.d)
+        for k, v in o.d.items():
+            d[k] = d.get(k, 0) + v
+        return Lin(d)
+
+    def __neg__(self):
+        return Lin({k: -v for k, v in self.d.items()})
+
+    def __sub__(self, o):
+        return self + (-o)
+
+    def scale(self, c):
+        return Lin({k: v * c for k, v in self.d.items()})
+
+
+class Prog:
+    def __init__(self, name):
+        self.name = name
+        self.stage = {}
+        self.level = {}          # for lin slots: level within the stage's linear phases
+        self.prods = []          # (stage, dst, x, y)
+        self.lins = []           # (stage, level, dst, terms)
+        self.ntemp = 0
+        self.outs = []
+
+    # ------------------------------------------------------------ slots
+    def inp(self, k):
+        s = IN_BASE + k
+        self.stage[s] = 0
+        return Lin({s: 1})
+
+    def const(self, k):
+        s = CONST_BASE + k
+        self.stage[s] = 0
+        return Lin({s: 1})
+
+    def _temp(self):
+        s = TEMP_BASE + self.ntemp
+        self.ntemp += 1
+        return s
+
+    def _avail(self, lin):
+        return max((self.stage[s] for s in lin.d), default=0)
+
+    def mat(self, lin, force=False):
+        if not force and len(lin.d) == 1 and list(lin.d.values())[0] == 1:
+            return lin
+        if len(lin.d) > MAXL:
+            items = list(lin.d.items())
+            head = self.mat(Lin(dict(items[:MAXL - 1])), force=True)
+            return self.mat(head + Lin(dict(items[MAXL - 1:])), force=force)
+        st = self._avail(lin)
+        lvl = 0
+        for s in lin.d:
+            if s in self.level and self.stage[s] == st:
+                lvl = max(lvl, self.level[s] + 1)
+        dst = self._temp()
+        self.lins.append((st, lvl, dst, lin))
+        self.stage[dst] = st
+        self.level[dst] = lvl
+        return Lin({dst: 1})
+
+    def mul(self, x, y):
+        if len(x.d) > MAXT:
+            x = self.mat(x)
+        if len(y.d) > MAXT:
+            y = self.mat(y)
+        st = 1 + max(self._avail(x), self._avail(y))
+        dst = self._temp()
+        self.prods.append((st, dst, x, y))
+        self.stage[dst] = st
+        return Lin({dst: 1})
+
+    def output(self, lins):
+        for lin in lins:
+            self.outs.append(list(self.mat(lin, force=True).d)[0])
+
+    # ------------------------------------------------------------ encoding
+    def encode(self):
+        nst = max([p[0] for p in self.prods] + [l[0] for l in self.lins] + [0])
+        phases = []
+        for s in range(nst + 1):
+            pr = [p for p in self.prods if p[0] == s]
+            if pr:
+                phases.append((0, pr))
+            lv = sorted({l[1] for l in self.lins if l[0] == s})
+            for v in lv:
+                phases.append((1, [l for l in self.lins if l[0] == s and l[1] == v]))
+        out = [len(phases), self.ntemp, len(self.outs)] + self.outs
+        out += [0] * (-len(out) % 8)          # records start 16-byte aligned
+        for kind, tasks in phases:
+            out += [kind, len(tasks)] + [0] * 6
+            for t in tasks:
+                if kind == 0:
+                    _, dst, x, y = t
+                    rec = [dst]
+                    for lin in (x, y):
+                        terms = list(lin.d.items())
+                        assert len(terms) <= MAXT
+                        assert sum(abs(c) for _, c in terms) <= 64  # lazy reduction bound (lb_wave.h)
+                        assert all(abs(c) <= 7 for _, c in terms)
+                        for k in range(MAXT):
+                            rec += list(terms[k]) if k < len(terms) else [0, 0]
+                    rec += [0] * (PREC - len(rec))
+                else:
+                    _, _, dst, lin = t
+                    terms = list(lin.d.items())
+                    assert len(terms) <= MAXL
+                    assert sum(abs(c) for _, c in terms) <= 64
+                    assert all(abs(c) <= 7 for _, c in terms)
+                    rec = [dst]
+                    for k in range(MAXL):
+                        rec += list(terms[k]) if k < len(terms) else [0, 0]
+                    rec += [0] * (LREC - len(rec))
+                out += rec
+        for v in out:
+            assert -32768 <= v < 32768
+        return out
+
+
+# ------------------------------------------------------------ traced tower (mirrors lb_field.h)
+class T:
+    """Tower ops over a Prog; Fp values are Lin, Fp2 = (Lin, Lin), Fp6 = 3-tuple, Fp12 = 2-tuple."""
+
+    def __init__(self, pg):
+        self.pg = pg
+
+    def m(self, a, b):
+        return self.pg.mul(a, b)
+
+    # Fp2
+    def f2add(self, a, b): return (a[0] + b[0], a[1] + b[1])
+    def f2sub(self, a, b): return (a[0] - b[0], a[1] - b[1])
+    def f2neg(self, a): return (-a[0], -a[1])
+    def f2conj(self, a): return (a[0], -a[1])
+    def f2dbl(self, a): return (a[0].scale(2), a[1].scale(2))
+    def f2mul3(self, a): return (a[0].scale(3), a[1].scale(3))
+    def f2xi(self, a): return (a[0] - a[1], a[0] + a[1])
+
+    def f2mul(self, a, b):
+        t0 = self.m(a[0], b[0])
+        t1 = self.m(a[1], b[1])
+        t2 = self.m(a[0] + a[1], b[0] + b[1])
+        return (t0 - t1, t2 - t0 - t1)
+
+    def f2sqr(self, a):
+        t0 = self.m(a[0] + a[1], a[0] - a[1])
+        t1 = self.m(a[0], a[1])
+        return (t0, t1.scale(2))
+
+    def f2mulfp(self, a, s):
+        return (self.m(a[0], s), self.m(a[1], s))
+
+    def f2mat(self, a):
+        return (self.pg.mat(a[0]), self.pg.mat(a[1]))
+
+    # Fp6
+    def f6add(self, a, b): return tuple(self.f2add(x, y) for x, y in zip(a, b))
+    def f6sub(self, a, b): return tuple(self.f2sub(x, y) for x, y in zip(a, b))
+    def f6neg(self, a): return tuple(self.f2neg(x) for x in a)
+    def f6mulv(self, a): return (self.f2xi(a[2]), a[0], a[1])
+
+    def f6mul(self, a, b):
+        t0 = self.f2mul(a[0], b[0])
+        t1 = self.f2mul(a[1], b[1])
+        t2 = self.f2mul(a[2], b[2])
+        c0 = self.f2add(self.f2xi(self.f2sub(self.f2sub(self.f2mul(self.f2add(a[1], a[2]), self.f2add(b[1], b[2])), t1), t2)), t0)
+        c1 = self.f2add(self.f2sub(self.f2sub(self.f2mul(self.f2add(a[0], a[1]), self.f2add(b[0], b[1])), t0), t1), self.f2xi(t2))
+        c2 = self.f2add(self.f2sub(self.f2sub(self.f2mul(self.f2add(a[0], a[2]), self.f2add(b[0], b[2])), t0), t2), t1)
+        return (c0, c1, c2)
+
+    def f6mul01(self, a, b0, b1):
+        t0 = self.f2mul(a[0], b0)
+        t1 = self.f2mul(a[1], b1)
+        c0 = self.f2add(self.f2xi(self.f2mul(a[2], b1)), t0)
+        c1 = self.f2sub(self.f2sub(self.f2mul(self.f2add(a[0], a[1]), self.f2add(b0, b1)), t0), t1)
+        c2 = self.f2add(self.f2mul(a[2], b0), t1)
+        return (c0, c1, c2)
+
+    def f6mul1(self, a, b1):
+        return (self.f2xi(self.f2mul(a[2], b1)), self.f2mul(a[0], b1), self.f2mul(a[1], b1))
+
+    # Fp12
+    def f12mul(self, a, b):
+        t0 = self.f6mul(a[0], b[0])
+        t1 = self.f6mul(a[1], b[1])
+        c1 = self.f6sub(self.f6sub(self.f6mul(self.f6add(a[0], a[1]), self.f6add(b[0], b[1])), t0), t1)
+        c0 = self.f6add(t0, self.f6mulv(t1))
+        return (c0, c1)
+
+    def f12sqr(self, a):
+        t = self.f6mul(a[0], a[1])
+        c0 = self.f6mul(self.f6add(a[0], a[1]), self.f6add(a[0], self.f6mulv(a[1])))
+        c0 = self.f6sub(self.f6sub(c0, t), self.f6mulv(t))
+        return (c0, self.f6add(t, t))
+
+    def f12mulline(self, a, l0, l2, l3):
+        t0 = self.f6mul01(a[0], l0, l2)
+        t1 = self.f6mul1(a[1], l3)
+        c1 = self.f6sub(self.f6sub(self.f6mul01(self.f6add(a[0], a[1]), l0, self.f2add(l2, l3)), t0), t1)
+        c0 = self.f6add(t0, self.f6mulv(t1))
+        return (c0, c1)
+
+    def f12mat(self, a):
+        return tuple(tuple(self.f2mat(x) for x in h) for h in a)
+
+
+def fp12_in(pg, base):
+    """12 consecutive input slots in tower order (c0.c0.c0, c0.c0.c1, c0.c1.c0, ...)."""
+    v = [pg.inp(base + k) for k in range(12)]
+    return ((v[0], v[1]), (v[2], v[3]), (v[4], v[5])), ((v[6], v[7]), (v[8], v[9]), (v[10], v[11]))
+
+
+def fp12_flat(a):
+    return [c for h in a for x in h for c in x]
+
+
+# ------------------------------------------------------------ Miller steps (mirror lb_pairing.h)
+def miller_dbl(t, T, xP, yP):
+    X, Y, Z = T
+    b3 = (t.pg.const(C_B3), t.pg.const(C_B3 + 1))
+    inv2 = t.pg.const(C_INV2)
+    A = t.f2mul(X, Y)
+    B = t.f2mat(t.f2sqr(Y))
+    C = t.f2mat(t.f2sqr(Z))
+    E = t.f2mat(t.f2mul(b3, C))
+    F = t.f2mul3(E)
+    G = t.f2add(B, F)
+    H = t.f2mat(t.f2sub(t.f2sqr(t.f2add(Y, Z)), t.f2add(B, C)))
+    XX3 = t.f2mul3(t.f2sqr(X))
+    l0 = t.f2sub(B, E)
+    l2 = t.f2neg(t.f2mulfp(t.f2mat(XX3), xP))
+    l3 = t.f2mulfp(H, yP)
+    A2 = t.f2mulfp(t.f2mat(A), inv2)
+    G2 = t.f2mulfp(t.f2mat(G), inv2)
+    X3 = t.f2mul(t.f2mat(A2), t.f2sub(B, F))
+    Y3 = t.f2sub(t.f2sqr(t.f2mat(G2)), t.f2mul3(t.f2sqr(E)))
+    Z3 = t.f2mul(B, H)
+    return (X3, Y3, Z3), (l0, l2, l3)
+
+
+def miller_add(t, T, Q, xP, yP):
+    X, Y, Z = T
+    xq, yq = Q
+    theta = t.f2mat(t.f2sub(Y, t.f2mul(yq, Z)))
+    lam = t.f2mat(t.f2sub(X, t.f2mul(xq, Z)))
+    l0 = t.f2sub(t.f2mul(theta, xq), t.f2mul(lam, yq))
+    l2 = t.f2neg(t.f2mulfp(theta, xP))
+    l3 = t.f2mulfp(lam, yP)
+    C = t.f2sqr(theta)
+    D = t.f2mat(t.f2sqr(lam))
+    E = t.f2mat(t.f2mul(lam, D))
+    F = t.f2mul(Z, t.f2mat(C))
+    G = t.f2mat(t.f2mul(X, D))
+    H = t.f2mat(t.f2sub(t.f2add(E, F), t.f2dbl(G)))
+    X3 = t.f2mul(lam, H)
+    Y3 = t.f2sub(t.f2mul(theta, t.f2sub(G, H)), t.f2mul(E, Y))
+    Z3 = t.f2mul(Z, E)
+    return (X3, Y3, Z3), (l0, l2, l3)
+
+
+def build_programs():
+    progs = {}
+    # MUL12: a = IN[0..12), b = IN[12..24)
+    pg = Prog("MUL12")
+    t = T(pg)
+    pg.output(fp12_flat(t.f12mul(fp12_in(pg, 0), fp12_in(pg, 12))))
+    progs["MUL12"] = pg
+    # SQR12
+    pg = Prog("SQR12")
+    t = T(pg)
+    pg.output(fp12_flat(t.f12sqr(fp12_in(pg, 0))))
+    progs["SQR12"] = pg
+    # DBL_STEP: f = IN[0..12), T = IN[12..18) (X.c0 X.c1 Y.c0 Y.c1 Z.c0 Z.c1), P = IN[18..20)
+    pg = Prog("DBL_STEP")
+    t = T(pg)
+    f = fp12_in(pg, 0)
+    Tt = tuple((pg.inp(12 + 2 * k), pg.inp(13 + 2 * k)) for k in range(3))
+    xP, yP = pg.inp(18), pg.inp(19)
+    T2, (l0, l2, l3) = miller_dbl(t, Tt, xP, yP)
+    l0, l2, l3 = t.f2mat(l0), t.f2mat(l2), t.f2mat(l3)
+    f2 = t.f12mat(t.f12sqr(f))
+    pg.output(fp12_flat(t.f12mulline(f2, l0, l2, l3)) + [c for x in T2 for c in x])
+    progs["DBL_STEP"] = pg
+    # ADD_STEP: f = IN[0..12), T = IN[12..18), Q = IN[18..22) (xq.c0 xq.c1 yq.c0 yq.c1), P = IN[22..24)
+    pg = Prog("ADD_STEP")
+    t = T(pg)
+    f = fp12_in(pg, 0)
+    Tt = tuple((pg.inp(12 + 2 * k), pg.inp(13 + 2 * k)) for k in range(3))
+    Q = ((pg.inp(18), pg.inp(19)), (pg.inp(20), pg.inp(21)))
+    xP, yP = pg.inp(22), pg.inp(23)
+    T2, (l0, l2, l3) = miller_add(t, Tt, Q, xP, yP)
+    l0, l2, l3 = t.f2mat(l0), t.f2mat(l2), t.f2mat(l3)
+    pg.output(fp12_flat(t.f12mulline(f, l0, l2, l3)) + [c for x in T2 for c in x])
+    progs["ADD_STEP"] = pg
+    # FROB: a^p, coefficient of w^k multiplied by conj(.) * FROB1_k (lb_field.h fp12_frob)
+    pg = Prog("FROB")
+    t = T(pg)
+    a = fp12_in(pg, 0)
+    wk = [a[0][0], a[1][0], a[0][1], a[1][1], a[0][2], a[1][2]]
+    r = [t.f2conj(wk[0])]
+    for k in range(1, 6):
+        ck = (pg.const(C_FROB1 + 2 * (k - 1)), pg.const(C_FROB1 + 2 * (k - 1) + 1))
+        r.append(t.f2mul(t.f2conj(wk[k]), ck))
+    res = ((r[0], r[2], r[4]), (r[1], r[3], r[5]))
+    pg.output(fp12_flat(res))
+    progs["FROB"] = pg
+    pg = Prog("FROB2")
+    t = T(pg)
+    a = fp12_in(pg, 0)
+    wk = [a[0][0], a[1][0], a[0][1], a[1][1], a[0][2], a[1][2]]
+    r = [wk[0]]
+    for k in range(1, 6):
+        r.append(t.f2mulfp(wk[k], pg.const(C_FROB2 + k - 1)))
+    res = ((r[0], r[2], r[4]), (r[1], r[3], r[5]))
+    pg.output(fp12_flat(res))
+    progs["FROB2"] = pg
+    return progs
+
+
+# ------------------------------------------------------------ reference evaluation (big ints)
+def run_encoded(code, slots):
+    """Interpret an encoded program over a dict slot -> int (mod P)."""
+    n_ph, n_temp, n_out = code[0], code[1], code[2]
+    outs = code[3:3 + n_out]
+    pos = 3 + n_out
+    pos += -pos % 8
+    S = dict(slots)
+
+    def lin(rec, off, n):
+        acc = 0
+        for k in range(n):
+            s, c = rec[off + 2 * k], rec[off + 2 * k + 1]
+            if c:
+                acc += c * S[s]
+        return acc % P
+
+    for _ in range(n_ph):
+        kind, n = code[pos], code[pos + 1]
+        pos += 8
+        rs = PREC if kind == 0 else LREC
+        new = {}
+        for k in range(n):
+            rec = code[pos + k * rs: pos + (k + 1) * rs]
+            if kind == 0:
+                new[rec[0]] = lin(rec, 1, MAXT) * lin(rec, 1 + 2 * MAXT, MAXT) % P
+            else:
+                new[rec[0]] = lin(rec, 1, MAXL)
+        S.update(new)
+        pos += n * rs
+    return [S[o] for o in outs]
+
+
+def _ref_checks(progs, codes):
+    sys.path.insert(0, ROOT)
+    from oracle import bls_oracle as o
+    rnd = random.Random(7)
+    consts = {}
+    b3 = (12, 12)
+    consts[CONST_BASE + C_B3], consts[CONST_BASE + C_B3 + 1] = b3
+    consts[CONST_BASE + C_INV2] = pow(2, P - 2, P)
+    xi = (1, 1)
+    for k in range(1, 6):
+        g = o.f2_pow(xi, k * (P - 1) // 6)
+        consts[CONST_BASE + C_FROB1 + 2 * (k - 1)], consts[CONST_BASE + C_FROB1 + 2 * (k - 1) + 1] = g
+        g2 = o.f2_pow(xi, k * (P * P - 1) // 6)
+        consts[CONST_BASE + C_FROB2 + k - 1] = g2[0]
+
+    def f12_from_flat(v):
+        # tower order -> oracle's representation via its own coefficient helper (w-basis coeffs)
+        c = [(v[0], v[1]), (v[6], v[7]), (v[2], v[3]), (v[8], v[9]), (v[4], v[5]), (v[10], v[11])]
+        return o.f12_from_f2_coeffs(c)
+
+    for _ in range(3):
+        a = [rnd.randrange(P) for _ in range(12)]
+        b = [rnd.randrange(P) for _ in range(12)]
+        S = dict(consts)
+        S.update({IN_BASE + k: a[k] for k in range(12)})
+        S.update({IN_BASE + 12 + k: b[k] for k in range(12)})
+        got = run_encoded(codes["MUL12"], S)
+        assert f12_from_flat(got) == o.f12_mul(f12_from_flat(a), f12_from_flat(b)), "MUL12"
+        got = run_encoded(codes["SQR12"], S)
+        assert f12_from_flat(got) == o.f12_sqr(f12_from_flat(a)), "SQR12"
+        got = run_encoded(codes["FROB"], S)
+        assert f12_from_flat(got) == o.f12_pow(f12_from_flat(a), P), "FROB"
+        got = run_encoded(codes["FROB2"], S)
+        assert f12_from_flat(got) == o.f12_pow(f12_from_flat(a), P * P), "FROB2"
+    # full pairing through the step programs vs the oracle: FE(ML)^... compare e(P,Q)^3 via
+    # the oracle final exponentiation of our Miller value (ours differs from the oracle's
+    # Miller value by Fp4 factors, which the final exponentiation removes)
+    sk = 0x1234567
+    Pp = o.sk_to_pk(sk)
+    Qq = o.hash_to_g2(b"\x07" * 32)
+    f = [1] + [0] * 11
+    Tx, Ty, Tz = Qq[0], Qq[1], (1, 0)
+    xabs = 0xD201000000010000
+    for i in range(62, -1, -1):
+        S = dict(consts)
+        vals = f + [Tx[0], Tx[1], Ty[0], Ty[1], Tz[0], Tz[1], Pp[0], Pp[1]]
+        S.update({IN_BASE + k: v for k, v in enumerate(vals)})
+        out = run_encoded(codes["DBL_STEP"], S)
+        f, (Tx, Ty, Tz) = out[:12], ((out[12], out[13]), (out[14], out[15]), (out[16], out[17]))
+        if (xabs >> i) & 1:
+            S = dict(consts)
+            vals = f + [Tx[0], Tx[1], Ty[0], Ty[1], Tz[0], Tz[1], Qq[0][0], Qq[0][1], Qq[1][0], Qq[1][1], Pp[0], Pp[1]]
+            S.update({IN_BASE + k: v for k, v in enumerate(vals)})
+            out = run_encoded(codes["ADD_STEP"], S)
+            f, (Tx, Ty, Tz) = out[:12], ((out[12], out[13]), (out[14], out[15]), (out[16], out[17]))
+    ml = o.f12_conj(f12_from_flat(f))
+    e = o.pairing(Pp, Qq)
+    assert o.final_exponentiation(ml) == e, "Miller step programs"
+
+
+def main():
+    progs = build_programs()
+    codes = {k: v.encode() for k, v in progs.items()}
+    _ref_checks(progs, codes)
+    lines = ["// Generated by tools/gen_wave_programs.py -- do not edit.",
+             "// Wave-cooperative programs (see the generator's docstring for the encoding).",
+             "#pragma once", "#include <stdint.h>", "",
+             f"#define LBW_MAXT {MAXT}", f"#define LBW_MAXL {MAXL}", f"#define LBW_PREC {PREC}",
+             f"#define LBW_LREC {LREC}",
+             f"#define LBW_IN {IN_BASE}", f"#define LBW_CONST {CONST_BASE}", f"#define LBW_TEMP {TEMP_BASE}",
+             f"#define LBW_C_B3 {C_B3}", f"#define LBW_C_INV2 {C_INV2}", f"#define LBW_C_FROB1 {C_FROB1}",
+             f"#define LBW_C_FROB2 {C_FROB2}", f"#define LBW_N_CONST {N_CONST}"]
+    maxtemp = 0
+    for name, code in codes.items():
+        pg = progs[name]
+        maxtemp = max(maxtemp, pg.ntemp)
+        nph = code[0]
+        lines.append(f"// {name}: {len(pg.prods)} products, {len(pg.lins)} linear tasks, {nph} phases, "
+                     f"{pg.ntemp} temps")
+        body = ", ".join(str(v) for v in code)
+        lines.append(f"static __device__ const int16_t __attribute__((aligned(16))) LBW_{name}[{len(code)}] = {{{body}}};")
+    lines.append(f"#define LBW_MAX_TEMPS {maxtemp}")
+    out = os.path.join(ROOT, "lodestar_amd", "csrc", "lb_wave_progs.h")
+    with open(out, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    for name, pg in progs.items():
+        print(f"{name}: {len(pg.prods)} products, {len(pg.lins)} lins, {codes[name][0]} phases, {pg.ntemp} temps")
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    main()
