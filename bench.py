@@ -55,16 +55,21 @@ def stage_work(counts, packed):
     m = 1
     while m < packed.n_jobs:
         m *= 2
-    blind = np.where(k == 1, c["pk_blind_k1"], c["pk_blind_k_base"] + c["pk_blind_per_extra_key"] * k).sum()
+    n_keys = int(packed.pk_off[-1])
     return {
         "decode_sigs": n * c["decode_sigs"],
         "hash_map": 2 * n * c["hash_map"],
         "hash_finish": n * c["hash_finish"],
-        "pk_blind": float(blind),
+        "pk_chunks": n_keys * c["pk_key"],
+        "pk_blind": n * c["g1_blind"],
+        "sig_blind": n * c["g2_blind"],
         "miller": n * c["miller"],
-        "job_leaves": float(((sets_per_job - 1).clip(0) * c["fp12_mul"] + sets_per_job * c["g2_add"]).sum()),
-        "tree_up": (m - 1) * (c["fp12_mul"] + c["g2_add"]),
-        "root_check": c["node_check"],
+        "job_leaves_P": float(((sets_per_job - 1).clip(0) * c["fp12_mul"]).sum()),
+        "tree_up_P": (m - 1) * c["fp12_mul"],
+        "job_leaves_S": float((sets_per_job * c["g2_add"]).sum()),
+        "tree_up_S": (m - 1) * c["g2_add"],
+        "ml_S": c["ml_S"],
+        "root_check": c["final_exp"] + c["fp12_mul"],
     }
 
 
@@ -82,10 +87,11 @@ def roofline(counts, packed, stage_ms):
                       "frac": round(fm * mac / t / 1e12 / peak, 4)}
     dom = max(per, key=lambda k: per[k]["ms"])
     ach = per[dom]["tmac_s"]
+    wall = stage_ms.get("total") or sum(stage_ms.values())
     return {"bound": "valu-int", "kernel": "k_" + dom, "achieved": ach, "peak": peak,
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": None,
-            "whole_pipeline_frac": round(sum(work.values()) * mac / (sum(stage_ms.values()) * 1e-3) / 1e12 / peak, 4),
-            "stages": per}
+            "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
+            "device_ms": round(wall, 3), "stages": per}
 
 
 def main():

@@ -43,16 +43,38 @@ struct dbuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-const char* const kStageNames[] = {"decode_sigs", "hash_map", "hash_finish", "pk_blind", "miller",
-                                   "job_leaves",  "tree_up",  "root_check",  "bisect"};
-constexpr int kStages = 9;
+// Pipeline stages; (s1) / (s2) = the HIP stream a stage runs on.  s2 carries signature decode,
+// pubkey aggregation + blinding and the whole sum(r_i sig_i) branch; s1 carries hash_to_G2,
+// the per-set Miller loops and the product tree.  They join before the root check.
+enum {
+  ST_DECODE = 0,  // s2
+  ST_HASH_MAP,    // s1
+  ST_HASH_FIN,    // s1
+  ST_PK_CHUNKS,   // s2
+  ST_PK_BLIND,    // s2
+  ST_SIG_BLIND,   // s2
+  ST_MILLER,      // s1
+  ST_LEAVES_P,    // s1
+  ST_TREE_P,      // s1
+  ST_LEAVES_S,    // s2
+  ST_TREE_S,      // s2
+  ST_ML_S,        // s2
+  ST_ROOT,        // s1 (after joining s2)
+  ST_BISECT,      // s1
+  ST_TOTAL,
+  kStages
+};
+const char* const kStageNames[kStages] = {"decode_sigs", "hash_map",     "hash_finish", "pk_chunks",   "pk_blind",
+                                          "sig_blind",   "miller",       "job_leaves_P", "tree_up_P",  "job_leaves_S",
+                                          "tree_up_S",   "ml_S",         "root_check",  "bisect",      "total"};
 
 }  // namespace
 
 struct lb_batch {
   uint32_t n_jobs = 0, n_sets = 0, n_pks = 0;
   std::vector<uint32_t> job_off;  // host copy (bisection bookkeeping)
-  dbuf d_job_off, d_pk_off, d_pks, d_msgs, d_sigs, d_sig_sizes;
+  uint32_t n_chunks = 0;           // pubkey aggregation chunks (k_pk_chunks)
+  dbuf d_job_off, d_pk_off, d_pks, d_msgs, d_sigs, d_sig_sizes, d_set_chunk_off, d_chunk_lo;
   bool has_sizes = false;
   int device = 0;
   ~lb_batch() {
@@ -62,22 +84,26 @@ struct lb_batch {
     d_msgs.release();
     d_sigs.release();
     d_sig_sizes.release();
+    d_set_chunk_off.release();
+    d_chunk_lo.release();
   }
 };
 
 struct lb_engine {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // s1
+  hipStream_t stream2 = nullptr;  // s2
+  hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr;
   std::mutex mu;
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
-      nodes, verdict, parts, ok;
+      nodes, verdict, parts, ok, chunk_acc, chunk_status, fS;
   std::vector<uint64_t> h_scalars;
   // profiling
   bool profiling = false;
-  hipEvent_t ev[kStages + 1] = {};
+  hipEvent_t ev0[kStages] = {}, ev1[kStages] = {};
+  bool used[kStages] = {};
   float last_ms[kStages] = {};
-  float acc_ms[kStages] = {};
 };
 
 #define LB_HIP(call)                                                                        \
@@ -153,11 +179,18 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   LB_HIP(hipSetDevice(device));
   lb_engine* e = new lb_engine();
   e->device = device;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return LB_ERR_DEVICE;
   }
-  for (int i = 0; i <= kStages; i++) hipEventCreate(&e->ev[i]);
+  hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_s, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+  for (int i = 0; i < kStages; i++) {
+    hipEventCreate(&e->ev0[i]);
+    hipEventCreate(&e->ev1[i]);
+  }
   *out = e;
   return LB_OK;
 }
@@ -168,10 +201,17 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamSynchronize(e->stream);
   dbuf* bufs[] = {&e->scalars, &e->sig_aff, &e->sig_inf, &e->sig_status, &e->q, &e->h_aff, &e->rpk, &e->rsig,
                   &e->pk_status, &e->ml, &e->treeP, &e->treeS, &e->job_status, &e->nodes, &e->verdict, &e->parts,
-                  &e->ok};
+                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS};
   for (dbuf* b : bufs) b->release();
-  for (int i = 0; i <= kStages; i++)
-    if (e->ev[i]) hipEventDestroy(e->ev[i]);
+  for (int i = 0; i < kStages; i++) {
+    if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
+    if (e->ev1[i]) hipEventDestroy(e->ev1[i]);
+  }
+  hipEventDestroy(e->ev_g1);
+  hipEventDestroy(e->ev_s);
+  hipEventDestroy(e->ev_fork);
+  hipStreamSynchronize(e->stream2);
+  hipStreamDestroy(e->stream2);
   hipStreamDestroy(e->stream);
   delete e;
 }
@@ -221,7 +261,19 @@ int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offse
     if (r != hipSuccess || !bytes) return r;
     return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, e->stream);
   };
+  // chunk decomposition of every set's pubkey range (<= LB_PK_CHUNK keys per chunk)
+  std::vector<uint32_t> set_chunk_off(n_sets + 1), chunk_lo;
+  for (uint32_t i = 0; i < n_sets; i++) {
+    set_chunk_off[i] = (uint32_t)chunk_lo.size();
+    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK) chunk_lo.push_back(k);
+  }
+  set_chunk_off[n_sets] = (uint32_t)chunk_lo.size();
+  b->n_chunks = (uint32_t)chunk_lo.size();
+  chunk_lo.push_back(n_pks);  // chunk c ends where chunk c+1 starts (chunks never span sets:
+  // a set's last chunk ends at the next set's first key, which is its own first chunk start)
   hipError_t r = up(b->d_job_off, job_offsets, (size_t)(n_jobs + 1) * 4);
+  if (r == hipSuccess) r = up(b->d_set_chunk_off, set_chunk_off.data(), set_chunk_off.size() * 4);
+  if (r == hipSuccess) r = up(b->d_chunk_lo, chunk_lo.data(), chunk_lo.size() * 4);
   if (r == hipSuccess) r = up(b->d_pk_off, set_pk_offsets, (size_t)(n_sets + 1) * 4);
   if (r == hipSuccess) r = up(b->d_pks, pubkeys, (size_t)n_pks * 96);
   if (r == hipSuccess) r = up(b->d_msgs, signing_roots, (size_t)n_sets * 32);
@@ -247,7 +299,24 @@ uint32_t lb_batch_num_jobs(const lb_batch* b) { return b ? b->n_jobs : 0; }
 
 }  // extern "C"
 
-// Runs the per-set pipeline and builds the job product tree.  m = tree leaf count (pow2).
+// stage timing helpers (HIP events on the stage's own stream)
+struct stage_scope {
+  lb_engine* e;
+  int k;
+  hipStream_t st;
+  stage_scope(lb_engine* e_, int k_, hipStream_t st_) : e(e_), k(k_), st(st_) {
+    if (e->profiling) {
+      hipEventRecord(e->ev0[k], st);
+      e->used[k] = true;
+    }
+  }
+  ~stage_scope() {
+    if (e->profiling) hipEventRecord(e->ev1[k], st);
+  }
+};
+
+// Runs the per-set pipeline on two streams and builds both job trees; leaves fS and treeP
+// ready for the root check on s1.  m = tree leaf count (pow2).
 static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& m) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
   int st = fill_scalars(e, n, scalars);
@@ -268,44 +337,100 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->treeP.ensure((size_t)2 * m * sizeof(fp12)));
   LB_HIP(e->treeS.ensure((size_t)2 * m * sizeof(g2j)));
   LB_HIP(e->job_status.ensure((size_t)(nj ? nj : 1) * 4));
-  hipStream_t s = e->stream;
-  if (n) LB_HIP(hipMemcpyAsync(e->scalars.p, e->h_scalars.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
-  auto mark = [&](int k) {
-    if (e->profiling) hipEventRecord(e->ev[k], s);
-  };
-  mark(0);
-  if (n) {
-    hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s, n, b->d_sigs.as<uint8_t>(),
-                       b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
-                       e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
-    mark(1);
-    hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * n)), dim3(LB_TPB), 0, s, n, b->d_msgs.as<uint8_t>(),
-                       e->q.as<uint32_t>());
-    mark(2);
-    hipLaunchKernelGGL(k_hash_finish, dim3(nblk(n)), dim3(LB_TPB), 0, s, n, e->q.as<uint32_t>(),
-                       e->h_aff.as<uint32_t>());
-    mark(3);
-    hipLaunchKernelGGL(k_pk_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s, n, b->d_pk_off.as<uint32_t>(),
-                       b->d_pks.as<uint8_t>(), e->scalars.as<uint64_t>(), e->sig_aff.as<uint32_t>(),
-                       e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(), e->rpk.as<uint32_t>(),
-                       e->rsig.as<uint32_t>(), e->pk_status.as<int32_t>());
-    mark(4);
-    hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s, n, e->rpk.as<uint32_t>(),
-                       e->h_aff.as<uint32_t>(), e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(),
-                       e->ml.as<uint32_t>());
-    mark(5);
-  } else {
-    for (int k = 1; k <= 5; k++) mark(k);
+  LB_HIP(e->fS.ensure(sizeof(fp12)));
+  const uint32_t nc = b->n_chunks;
+  LB_HIP(e->chunk_acc.ensure((size_t)(nc ? nc : 1) * sizeof(g1j)));
+  LB_HIP(e->chunk_status.ensure((size_t)(nc ? nc : 1) * 4));
+  for (int k = 0; k < kStages; k++) e->used[k] = false;
+  hipStream_t s1 = e->stream, s2 = e->stream2;
+  if (e->profiling) {
+    hipEventRecord(e->ev0[ST_TOTAL], s1);
+    e->used[ST_TOTAL] = true;
   }
-  hipLaunchKernelGGL(k_job_leaves, dim3(nblk(m)), dim3(LB_TPB), 0, s, nj, n, m, b->d_job_off.as<uint32_t>(),
-                     e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>(),
-                     e->rsig.as<uint32_t>(), e->treeP.as<uint32_t>(), e->treeS.as<uint32_t>(),
-                     e->job_status.as<int32_t>());
-  mark(6);
-  for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
-    hipLaunchKernelGGL(k_tree_up, dim3(lo + nblk(lo)), dim3(64), 0, s, m, lo, e->treeP.as<uint32_t>(),
+  if (n) LB_HIP(hipMemcpyAsync(e->scalars.p, e->h_scalars.data(), (size_t)n * 8, hipMemcpyHostToDevice, s1));
+  // fork: s2 starts after s1's scalar upload
+  LB_HIP(hipEventRecord(e->ev_fork, s1));
+  LB_HIP(hipStreamWaitEvent(s2, e->ev_fork, 0));
+  if (n) {
+    // ---- s2: signatures, pubkeys, r*PK
+    {
+      stage_scope sc(e, ST_DECODE, s2);
+      hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
+                         b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
+                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+    }
+    {
+      stage_scope sc(e, ST_PK_CHUNKS, s2);
+      if (nc)
+        hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
+                           b->d_pks.as<uint8_t>(), e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>());
+    }
+    {
+      stage_scope sc(e, ST_PK_BLIND, s2);
+      hipLaunchKernelGGL(k_pk_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, nc, b->d_set_chunk_off.as<uint32_t>(),
+                         e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), b->d_pk_off.as<uint32_t>(),
+                         e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
+    }
+    LB_HIP(hipEventRecord(e->ev_g1, s2));
+    // ---- s1: hash_to_G2
+    {
+      stage_scope sc(e, ST_HASH_MAP, s1);
+      hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(),
+                         e->q.as<uint32_t>());
+    }
+    {
+      stage_scope sc(e, ST_HASH_FIN, s1);
+      hipLaunchKernelGGL(k_hash_finish, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->q.as<uint32_t>(),
+                         e->h_aff.as<uint32_t>());
+    }
+    // ---- s2: the sum(r_i sig_i) branch, overlapped with the Miller loops
+    {
+      stage_scope sc(e, ST_SIG_BLIND, s2);
+      hipLaunchKernelGGL(k_sig_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
+                         e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(),
+                         e->rsig.as<uint32_t>());
+    }
+    // ---- s1: Miller loops (need r*PK and the statuses from s2)
+    LB_HIP(hipStreamWaitEvent(s1, e->ev_g1, 0));
+    {
+      stage_scope sc(e, ST_MILLER, s1);
+      hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rpk.as<uint32_t>(),
+                         e->h_aff.as<uint32_t>(), e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(),
+                         e->ml.as<uint32_t>());
+    }
+  } else {
+    LB_HIP(hipEventRecord(e->ev_g1, s2));
+  }
+  // ---- s2: S tree and ML(-G1, S_root)
+  {
+    stage_scope sc(e, ST_LEAVES_S, s2);
+    hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(m)), dim3(LB_TPB), 0, s2, nj, n, m, b->d_job_off.as<uint32_t>(),
+                       e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->rsig.as<uint32_t>(),
                        e->treeS.as<uint32_t>());
-  mark(7);
+  }
+  {
+    stage_scope sc(e, ST_TREE_S, s2);
+    for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
+      hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s2, m, lo, e->treeS.as<uint32_t>());
+  }
+  {
+    stage_scope sc(e, ST_ML_S, s2);
+    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, m, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
+  }
+  LB_HIP(hipEventRecord(e->ev_s, s2));
+  // ---- s1: P tree
+  {
+    stage_scope sc(e, ST_LEAVES_P, s1);
+    hipLaunchKernelGGL(k_job_leaves_P, dim3(nblk(m)), dim3(LB_TPB), 0, s1, nj, n, m, b->d_job_off.as<uint32_t>(),
+                       e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>(),
+                       e->treeP.as<uint32_t>(), e->job_status.as<int32_t>());
+  }
+  {
+    stage_scope sc(e, ST_TREE_P, s1);
+    for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
+      hipLaunchKernelGGL(k_tree_up_P, dim3(lo), dim3(64), 0, s1, m, lo, e->treeP.as<uint32_t>());
+  }
+  LB_HIP(hipStreamWaitEvent(s1, e->ev_s, 0));  // join
   LB_HIP(hipGetLastError());
   return LB_OK;
 }
@@ -325,16 +450,13 @@ static int32_t check_nodes(lb_engine* e, uint32_t m, const std::vector<uint32_t>
   return LB_OK;
 }
 
-static void finish_profile(lb_engine* e, bool bisected) {
+static void finish_profile(lb_engine* e) {
   if (!e->profiling) return;
-  hipEventSynchronize(e->ev[kStages]);
+  hipStreamSynchronize(e->stream2);
+  hipStreamSynchronize(e->stream);
   for (int k = 0; k < kStages; k++) {
     float ms = 0.f;
-    if (k == kStages - 1 && !bisected) {
-      e->last_ms[k] = 0.f;
-      continue;
-    }
-    hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]);
+    if (e->used[k]) hipEventElapsedTime(&ms, e->ev0[k], e->ev1[k]);
     e->last_ms[k] = ms;
   }
 }
@@ -348,63 +470,78 @@ extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* sc
   uint32_t m = 1;
   int32_t st = run_pipeline(e, b, scalars, m);
   if (st != LB_OK) return st;
+  // root verdict on s1 (after the join)
+  LB_HIP(e->verdict.ensure(4));
+  {
+    stage_scope sc(e, ST_ROOT, e->stream);
+    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
+                       e->fS.as<uint32_t>(), e->verdict.as<int32_t>());
+  }
+  LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(nj);
+  int32_t root_ok = 0;
   LB_HIP(hipMemcpyAsync(jst.data(), e->job_status.p, (size_t)nj * 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipMemcpyAsync(&root_ok, e->verdict.p, 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipStreamSynchronize(e->stream));
   // subtree "live job" counts, heap layout (leaves at [m, 2m))
   std::vector<uint32_t> live(2 * m, 0);
-  LB_HIP(hipStreamSynchronize(e->stream));
   for (uint32_t j = 0; j < nj; j++) live[m + j] = jst[j] == LB_OK ? 1u : 0u;
   for (uint32_t i = m - 1; i >= 1; i--) live[i] = live[2 * i] + live[2 * i + 1];
   for (uint32_t j = 0; j < nj; j++) out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
+  // bisection over the job tree below a failing root
   std::vector<uint32_t> cand;
   std::vector<int32_t> v;
-  if (live[1]) cand.push_back(1);
-  bool first = true, bisected = false;
-  while (!cand.empty()) {
-    st = check_nodes(e, m, cand, v);
-    if (st != LB_OK) return st;
-    if (first) {
-      if (e->profiling) hipEventRecord(e->ev[8], e->stream);
-      first = false;
+  if (live[1] && !root_ok) {
+    if (m == 1) {
+      out_job[0] = 0;
     } else {
-      bisected = true;
+      cand.push_back(2);
+      cand.push_back(3);
     }
-    std::vector<uint32_t> next;
-    for (size_t k = 0; k < cand.size(); k++) {
-      uint32_t c = cand[k];
-      if (v[k]) continue;  // verified: its live jobs stay 1
-      if (c >= m) {
-        out_job[c - m] = 0;
-        continue;
-      }
-      next.push_back(2 * c);
-      next.push_back(2 * c + 1);
-    }
-    // drop empty subtrees; when the failing subtrees are small, test their leaves directly
-    std::vector<uint32_t> nz;
-    uint64_t leaves = 0;
-    for (uint32_t c : next)
-      if (live[c]) {
-        nz.push_back(c);
-        leaves += live[c];
-      }
-    if (!nz.empty() && leaves <= 256) {
-      std::vector<uint32_t> lv;
-      for (uint32_t c : nz) {
-        uint32_t lo = c, hi = c;
-        while (lo < m) {
-          lo = 2 * lo;
-          hi = 2 * hi + 1;
-        }
-        for (uint32_t l = lo; l <= hi; l++)
-          if (live[l]) lv.push_back(l);
-      }
-      nz.swap(lv);
-    }
-    cand.swap(nz);
   }
-  if (e->profiling) hipEventRecord(e->ev[kStages], e->stream);
-  finish_profile(e, bisected);
+  {
+    stage_scope sc(e, ST_BISECT, e->stream);
+    while (!cand.empty()) {
+      // drop empty subtrees; when the failing subtrees are small, test their leaves directly
+      std::vector<uint32_t> nz;
+      uint64_t leaves = 0;
+      for (uint32_t c : cand)
+        if (live[c]) {
+          nz.push_back(c);
+          leaves += live[c];
+        }
+      if (!nz.empty() && leaves <= 256) {
+        std::vector<uint32_t> lv;
+        for (uint32_t c : nz) {
+          uint32_t lo = c, hi = c;
+          while (lo < m) {
+            lo = 2 * lo;
+            hi = 2 * hi + 1;
+          }
+          for (uint32_t l = lo; l <= hi; l++)
+            if (live[l]) lv.push_back(l);
+        }
+        nz.swap(lv);
+      }
+      if (nz.empty()) break;
+      st = check_nodes(e, m, nz, v);
+      if (st != LB_OK) return st;
+      std::vector<uint32_t> next;
+      for (size_t k = 0; k < nz.size(); k++) {
+        uint32_t c = nz[k];
+        if (v[k]) continue;  // verified: its live jobs stay 1
+        if (c >= m) {
+          out_job[c - m] = 0;
+          continue;
+        }
+        next.push_back(2 * c);
+        next.push_back(2 * c + 1);
+      }
+      cand.swap(next);
+    }
+  }
+  if (e->profiling) hipEventRecord(e->ev1[ST_TOTAL], e->stream);
+  finish_profile(e);
   return LB_OK;
 }
 
@@ -421,19 +558,19 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   int32_t st = run_pipeline(e, b, scalars, m);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
-  hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
-                     e->treeS.as<uint32_t>(), e->parts.as<uint8_t>());
+  {
+    stage_scope sc(e, ST_ROOT, e->stream);
+    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
+                       e->fS.as<uint32_t>(), e->parts.as<uint8_t>());
+  }
   LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(b->n_jobs);
   LB_HIP(hipMemcpyAsync(out576, e->parts.p, 576, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipMemcpyAsync(jst.data(), e->job_status.p, (size_t)b->n_jobs * 4, hipMemcpyDeviceToHost, e->stream));
-  if (e->profiling) {
-    hipEventRecord(e->ev[8], e->stream);
-    hipEventRecord(e->ev[9], e->stream);
-  }
+  if (e->profiling) hipEventRecord(e->ev1[ST_TOTAL], e->stream);
   LB_HIP(hipStreamSynchronize(e->stream));
   for (uint32_t j = 0; j < b->n_jobs; j++) out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
-  finish_profile(e, false);
+  finish_profile(e);
   return LB_OK;
 }
 

@@ -115,23 +115,18 @@ __global__ void __launch_bounds__(LB_TPB) k_hash_finish(uint32_t n, const uint32
 }
 
 // ---------------------------------------------------------------- pubkeys + blinding
-// pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
-__global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, const uint32_t* __restrict__ pk_off,
-                                                     const uint8_t* __restrict__ pks,
-                                                     const uint64_t* __restrict__ scalars,
-                                                     const uint32_t* __restrict__ sig_aff,
-                                                     const uint32_t* __restrict__ sig_inf,
-                                                     const int32_t* __restrict__ sig_status,
-                                                     uint32_t* __restrict__ rpk_aff,
-                                                     uint32_t* __restrict__ rsig,
-                                                     int32_t* __restrict__ pk_status) {
-  uint32_t i = lb_tid();
-  if (i >= n) return;
-  uint32_t a = pk_off[i], e = pk_off[i + 1];
-  int st = (a == e) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+// G1 aggregation (getAggregatedPubkey, utils.ts:5-16) is split into chunks of <= LB_PK_CHUNK
+// keys so a 512-key sync aggregate costs one chunk's latency plus a short combine instead of
+// 512 serial additions on one lane; chunk c covers pubkeys [chunk_lo[c], chunk_lo[c+1]) of one set.
+#define LB_PK_CHUNK 16
+__global__ void __launch_bounds__(LB_TPB) k_pk_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
+                                                      const uint8_t* __restrict__ pks, uint32_t* __restrict__ chunk_acc,
+                                                      int32_t* __restrict__ chunk_status) {
+  uint32_t c = lb_tid();
+  if (c >= nc) return;
+  uint32_t a = chunk_lo[c], e = chunk_lo[c + 1];
+  int st = LB_OK;
   g1j acc = jac_infinity<fp>();
-  bool single = (e - a) == 1;
-  g1a first;
   for (uint32_t k = a; k < e && st == LB_OK; k++) {
     uint8_t b[96];
     ld_bytes<96>(b, pks + (size_t)96 * k);
@@ -139,22 +134,55 @@ __global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, const uint32_t*
     bool inf;
     st = g1_deserialize96(b, p, inf);
     if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
-    if (k == a) first = p;
+  }
+  soa_st(chunk_acc, nc, c, acc);
+  chunk_status[c] = st;
+}
+
+// pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
+// r * PK for the Miller loop (critical path; the G2 side r * sig is k_sig_blind, off it).
+__global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
+                                                     const uint32_t* __restrict__ chunk_acc,
+                                                     const int32_t* __restrict__ chunk_status,
+                                                     const uint32_t* __restrict__ pk_off,
+                                                     const uint64_t* __restrict__ scalars,
+                                                     uint32_t* __restrict__ rpk_aff,
+                                                     int32_t* __restrict__ pk_status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
+  int st = (c0 == c1) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+  g1j acc = jac_infinity<fp>();
+  for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
+    st = chunk_status[c];
+    if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
   }
   if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
-  uint64_t r = scalars[i];
+  const bool single = (pk_off[i + 1] - pk_off[i]) == 1;
   g1a rp;
   rp.x = fp_zero();
   rp.y = fp_zero();
-  g2j rs = jac_infinity<fp2>();
   if (st == LB_OK) {
-    g1j rj = single ? jac_mul_u64(first, r) : jac_mul_u64_jac(acc, r);
+    // a single key's chunk sum is the affine point itself (Z = 1): use mixed additions
+    const uint64_t r = scalars[i];
+    g1j rj = single ? jac_mul_u64(g1a{acc.x, acc.y}, r) : jac_mul_u64_jac(acc, r);
     jac_to_aff(rp, rj);
-    if (sig_status[i] == LB_OK && sig_inf[i] == 0u) rs = jac_mul_u64(soa_ld<g2a>(sig_aff, n, i), r);
   }
   soa_st(rpk_aff, n, i, rp);
-  soa_st(rsig, n, i, rs);
   pk_status[i] = st;
+}
+
+// r * sig (Jacobian G2) for the aggregate-signature side of the batch equation
+__global__ void __launch_bounds__(LB_TPB) k_sig_blind(uint32_t n, const uint64_t* __restrict__ scalars,
+                                                      const uint32_t* __restrict__ sig_aff,
+                                                      const uint32_t* __restrict__ sig_inf,
+                                                      const int32_t* __restrict__ sig_status,
+                                                      uint32_t* __restrict__ rsig) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  g2j rs = jac_infinity<fp2>();
+  if (sig_status[i] == LB_OK && sig_inf[i] == 0u) rs = jac_mul_u64(soa_ld<g2a>(sig_aff, n, i), scalars[i]);
+  soa_st(rsig, n, i, rs);
 }
 
 // ---------------------------------------------------------------- Miller loops
@@ -175,70 +203,120 @@ __global__ void __launch_bounds__(LB_TPB) k_miller(uint32_t n, const uint32_t* _
 }
 
 // ---------------------------------------------------------------- per-job leaves
-// Job status follows maybeBatch.ts: all signatures are decoded first (first failing one
-// throws), then pubkeys are consumed in order by mul_n_aggregate.
-__global__ void __launch_bounds__(LB_TPB) k_job_leaves(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
-                                                       const uint32_t* __restrict__ job_off,
-                                                       const int32_t* __restrict__ sig_status,
-                                                       const int32_t* __restrict__ pk_status,
-                                                       const uint32_t* __restrict__ ml,
-                                                       const uint32_t* __restrict__ rsig,
-                                                       uint32_t* __restrict__ treeP,
-                                                       uint32_t* __restrict__ treeS,
-                                                       int32_t* __restrict__ job_status) {
+// Job status follows the reference's error precedence: aggregation / pubkey decoding happen
+// first (main thread getAggregatedPubkey, worker deserializeSet), then every signature is
+// decoded (maybeBatch.ts:18-25), then mul_n_aggregate rejects an infinite pubkey.
+__device__ __forceinline__ int job_status_of(uint32_t a, uint32_t e, const int32_t* sig_status, const int32_t* pk_status) {
+  int st = (a == e) ? LB_EMPTY_SIGNATURE_SET : LB_OK;
+  for (uint32_t i = a; i < e && st == LB_OK; i++)
+    if (pk_status[i] != LB_OK && pk_status[i] != LB_PK_IS_INFINITY) st = pk_status[i];
+  for (uint32_t i = a; i < e && st == LB_OK; i++)
+    if (sig_status[i] != LB_OK) st = sig_status[i];
+  for (uint32_t i = a; i < e && st == LB_OK; i++)
+    if (pk_status[i] != LB_OK) st = pk_status[i];
+  return st;
+}
+
+// P_j = prod ML_i over the job's sets (identity for a rejecting job) -> treeP leaf m + j
+__global__ void __launch_bounds__(LB_TPB) k_job_leaves_P(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
+                                                         const uint32_t* __restrict__ job_off,
+                                                         const int32_t* __restrict__ sig_status,
+                                                         const int32_t* __restrict__ pk_status,
+                                                         const uint32_t* __restrict__ ml, uint32_t* __restrict__ treeP,
+                                                         int32_t* __restrict__ job_status) {
   uint32_t j = lb_tid();
   if (j >= m) return;
   fp12 P = fp12_one();
-  g2j S = jac_infinity<fp2>();
-  int st = LB_OK;
   if (j < n_jobs) {
     uint32_t a = job_off[j], e = job_off[j + 1];
-    // error precedence of the reference: aggregation / pubkey decoding happen first
-    // (main thread getAggregatedPubkey, worker deserializeSet), then every signature is
-    // decoded (maybeBatch.ts:18-25), then mul_n_aggregate rejects an infinite pubkey.
-    if (a == e) st = LB_EMPTY_SIGNATURE_SET;
-    for (uint32_t i = a; i < e && st == LB_OK; i++)
-      if (pk_status[i] != LB_OK && pk_status[i] != LB_PK_IS_INFINITY) st = pk_status[i];
-    for (uint32_t i = a; i < e && st == LB_OK; i++)
-      if (sig_status[i] != LB_OK) st = sig_status[i];
-    for (uint32_t i = a; i < e && st == LB_OK; i++)
-      if (pk_status[i] != LB_OK) st = pk_status[i];
-    if (st == LB_OK) {
+    int st = job_status_of(a, e, sig_status, pk_status);
+    if (st == LB_OK)
       for (uint32_t i = a; i < e; i++) {
         fp12 f = soa_ld<fp12>(ml, n_sets, i);
         P = (i == a) ? f : fp12_mul(P, f);
-        S = jac_add(S, soa_ld<g2j>(rsig, n_sets, i));
       }
-    }
     job_status[j] = st;
   }
-  if (st != LB_OK) {
-    P = fp12_one();
-    S = jac_infinity<fp2>();
-  }
   soa_st(treeP, 2 * m, m + j, P);
+}
+
+// S_j = sum r_i sig_i over the job's sets (identity for a rejecting job) -> treeS leaf m + j
+__global__ void __launch_bounds__(LB_TPB) k_job_leaves_S(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
+                                                         const uint32_t* __restrict__ job_off,
+                                                         const int32_t* __restrict__ sig_status,
+                                                         const int32_t* __restrict__ pk_status,
+                                                         const uint32_t* __restrict__ rsig, uint32_t* __restrict__ treeS) {
+  uint32_t j = lb_tid();
+  if (j >= m) return;
+  g2j S = jac_infinity<fp2>();
+  if (j < n_jobs) {
+    uint32_t a = job_off[j], e = job_off[j + 1];
+    if (job_status_of(a, e, sig_status, pk_status) == LB_OK)
+      for (uint32_t i = a; i < e; i++) S = jac_add(S, soa_ld<g2j>(rsig, n_sets, i));
+  }
   soa_st(treeS, 2 * m, m + j, S);
 }
 
 // Product tree over jobs, one level: nodes [lo, 2 lo), node i = node 2i (x) node 2i+1.
-// Blocks [0, lo): one wave per node multiplies the Fp12 children cooperatively (MUL12 program).
-// Blocks [lo, lo + ceil(lo/64)): one lane per node adds the G2 children (Jacobian).
-__global__ void __launch_bounds__(64) k_tree_up(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP,
-                                                uint32_t* __restrict__ treeS) {
+// One wave per node multiplies the Fp12 children cooperatively (MUL12 program).
+__global__ void __launch_bounds__(64) k_tree_up_P(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP) {
   __shared__ fp S[LBW_SLOTS];
-  if (blockIdx.x < lo) {
-    uint32_t i = lo + blockIdx.x;
-    w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
-    w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
-    w_mul(S, LBW_A(2), LBW_A(0), LBW_A(1));
-    w_store_soa12(S, LBW_A(2), treeP, 2 * m, i);
-  } else {
-    uint32_t t = (blockIdx.x - lo) * 64 + threadIdx.x;
-    if (t >= lo) return;
-    uint32_t i = lo + t;
-    g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
-    soa_st(treeS, 2 * m, i, s);
+  uint32_t i = lo + blockIdx.x;
+  w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
+  w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
+  w_mul(S, LBW_A(2), LBW_A(0), LBW_A(1));
+  w_store_soa12(S, LBW_A(2), treeP, 2 * m, i);
+}
+
+// G2 sum tree, one level, one lane per node (Jacobian additions)
+__global__ void __launch_bounds__(LB_TPB) k_tree_up_S(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeS) {
+  uint32_t t = lb_tid();
+  if (t >= lo) return;
+  uint32_t i = lo + t;
+  g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
+  soa_st(treeS, 2 * m, i, s);
+}
+
+// fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
+// computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
+__global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
+  __shared__ fp S[LBW_SLOTS];
+  __shared__ int s_inf;
+  const int lane = threadIdx.x;
+  w_init_consts(S);
+  if (lane == 0) {
+    g2j Sj = soa_ld<g2j>(treeS, 2 * m, 1);
+    s_inf = jac_is_inf(Sj) ? 1 : 0;
+    if (!s_inf) {
+      g2a a;
+      jac_to_aff(a, Sj);
+      S[LBW_PT + 0] = fp_load(LB_G1X);
+      S[LBW_PT + 1] = fp_load(LB_G1NEGY);
+      S[LBW_PT + 2] = a.x.c0;
+      S[LBW_PT + 3] = a.x.c1;
+      S[LBW_PT + 4] = a.y.c0;
+      S[LBW_PT + 5] = a.y.c1;
+    }
   }
+  w_sync();
+  if (s_inf)
+    w_set_one(S, LBW_A(7));
+  else
+    w_miller(S, LBW_A(7));
+  w_store_soa12(S, LBW_A(7), fS, 1, 0);
+}
+
+// root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
+__global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                   const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict) {
+  __shared__ fp S[LBW_SLOTS];
+  w_init_consts(S);
+  w_load_soa12(S, LBW_A(0), treeP, 2 * m, 1);
+  w_load_soa12(S, LBW_A(7), fS, 1, 0);
+  w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
+  w_final_exp(S, LBW_A(0), LBW_A(0));
+  bool one = w_is_one(S, LBW_A(0));
+  if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
 
 // One wave per checked node: verdict = FE(P * ML(-G1, S)) == 1   (Pairing.finalverify)
@@ -254,12 +332,14 @@ __global__ void __launch_bounds__(64) k_node_check(uint32_t m, uint32_t cnt, con
   if (threadIdx.x == 0) verdict[blockIdx.x] = one ? 1 : 0;
 }
 
-// root partial product as 576 bytes (multi-GPU exchange format)
+// root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
 __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
-                                                     const uint32_t* __restrict__ treeS, uint8_t* __restrict__ out576) {
+                                                     const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
   __shared__ fp S[LBW_SLOTS];
   w_init_consts(S);
-  w_node_partial(S, LBW_A(0), treeP, treeS, 2 * m, 1);
+  w_load_soa12(S, LBW_A(0), treeP, 2 * m, 1);
+  w_load_soa12(S, LBW_A(7), fS, 1, 0);
+  w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(S[LBW_A(0) + threadIdx.x]));
 }
 

@@ -54,6 +54,39 @@ unsigned long long cnt_pk_blind(const uint8_t* pks, int k, uint64_t r, const uin
   jac_mul_u64(s, r);
   return lb_count_mul;
 }
+// the two halves of blinding (k_pk_blind: r*PK + affine; k_sig_blind: r*sig)
+unsigned long long cnt_g1_blind(const uint8_t* pk96, uint64_t r) {
+  g1a p; bool inf;
+  g1_deserialize96(pk96, p, inf);
+  lb_count_mul = 0;
+  g1a rp;
+  jac_to_aff(rp, jac_mul_u64(p, r));
+  return lb_count_mul;
+}
+unsigned long long cnt_g2_blind(const uint8_t* sig96, uint64_t r) {
+  g2a s; bool inf;
+  g2_decompress96(sig96, s, inf);
+  lb_count_mul = 0;
+  jac_mul_u64(s, r);
+  return lb_count_mul;
+}
+unsigned long long cnt_pk_key(const uint8_t* pks, int k) {
+  lb_count_mul = 0;
+  g1j acc = jac_infinity<fp>();
+  for (int i = 0; i < k; i++) {
+    g1a p; bool inf;
+    g1_deserialize96(pks + 96 * i, p, inf);
+    acc = jac_add_aff(acc, p);
+  }
+  return lb_count_mul;
+}
+unsigned long long cnt_fe(void) {
+  fp12 f = fp12_one();
+  f.c1.c2.c0 = fp_one();
+  lb_count_mul = 0;
+  final_exponentiation(f);
+  return lb_count_mul;
+}
 unsigned long long cnt_miller(const uint8_t* pk96, const uint8_t* msg) {
   g1a p; bool inf;
   g1_deserialize96(pk96, p, inf);

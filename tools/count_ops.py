@@ -28,8 +28,11 @@ def main():
                     os.path.join(ROOT, "tests", "harness", "lb_count.cpp"), "-o", SO], check=True)
     L = ctypes.CDLL(SO)
     for f in ("cnt_decode", "cnt_hash_map", "cnt_hash_finish", "cnt_pk_blind", "cnt_miller", "cnt_fp12_mul",
-              "cnt_g2_add", "cnt_node_check"):
+              "cnt_g2_add", "cnt_node_check", "cnt_g1_blind", "cnt_g2_blind", "cnt_pk_key", "cnt_fe"):
         getattr(L, f).restype = ctypes.c_ulonglong
+    L.cnt_g1_blind.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    L.cnt_g2_blind.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+    L.cnt_pk_key.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.cnt_pk_blind.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_char_p]
     rnd = random.Random(5)
     sks = [o.interop_secret_key(i) for i in range(4)]
@@ -50,6 +53,10 @@ def main():
     fp12m = L.cnt_fp12_mul()
     g2add = L.cnt_g2_add(sigs[0])
     node = L.cnt_node_check(sigs[0])
+    g1b = avg([L.cnt_g1_blind(pks[0], rnd.getrandbits(64) | 1) for _ in range(16)])
+    g2b = avg([L.cnt_g2_blind(sigs[0], rnd.getrandbits(64) | 1) for _ in range(16)])
+    per_key = (L.cnt_pk_key(b"".join(pks[:4]), 4) - L.cnt_pk_key(pks[0], 1)) / 3
+    fe = L.cnt_fe()
     out = {
         "mac_per_fp_mul": 300,
         "peak_tmac_s": json.load(open(os.path.join(ROOT, "profiles", "r1_ubench_int.json")))["v_mad_u64_u32_Tops"],
@@ -64,6 +71,11 @@ def main():
             "miller": c["miller"],                    # per set
             "fp12_mul": fp12m, "g2_add": g2add,       # job_leaves / tree_up building blocks
             "node_check": node,                       # per checked tree node (ML + FE)
+            "pk_key": per_key,                        # k_pk_chunks: decode + add per pubkey
+            "g1_blind": g1b,                          # k_pk_blind per set (r*PK + affine)
+            "g2_blind": g2b,                          # k_sig_blind per set (r*sig)
+            "final_exp": fe,                          # k_root_check
+            "ml_S": c["miller"] + (node - fe - c["miller"] - fp12m),  # k_ml_S: ML + G2 affine
         },
         "items_per_set": {"decode_sigs": 1, "hash_map": 2, "hash_finish": 1, "pk_blind": 1, "miller": 1},
     }

@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 echo "== pytest"; timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-echo "== bench"; timeout -k 10 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1; rc=$?; tail -1 gpurun_out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step']); [print(k, v) for k, v in d['roofline']['stages'].items()]"; exit $rc
+echo "== bench"; timeout -k 10 600 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1; rc=$?; tail -1 gpurun_out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel'], r['frac'], r['whole_pipeline_frac'], r['device_ms']); [print(k, v) for k, v in r['stages'].items()]"; exit $rc
