@@ -79,10 +79,29 @@ def build_cpu_pool(force=False, verbose=True):
     return CPU_POOL
 
 
+UBENCH = ["fpmul_asm"]  # tools/ubench programs the GPU tests run (correctness of the asm Fp multiply)
+
+
+def build_ubench(force=False, verbose=True):
+    out = []
+    for name in UBENCH:
+        src = os.path.join(ROOT, "tools", "ubench", name + ".hip")
+        dst = os.path.join(ROOT, "tools", "ubench", name)
+        if force or _stale(dst, _deps() + [src]):
+            cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-result", "-Wno-unused-value",
+                   "-I" + INC, "-I" + CSRC, src, "-o", dst]
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+        out.append(dst)
+    return out
+
+
 def build_all(force=False):
     build_lib(force)
     build_harness(force)
     build_cpu_pool(force)
+    build_ubench(force)
 
 
 if __name__ == "__main__":

@@ -9,6 +9,7 @@
 #pragma once
 #include "lb_common.h"
 #include "lb_consts.h"
+#include "lb_fpmul_gfx950.h"
 
 struct fp {
   uint32_t v[12];
@@ -164,7 +165,15 @@ __device__ __forceinline__ fp fp_unpack(lb_v16u a) {
   return r;
 }
 static __device__ __attribute__((noinline)) lb_v16u fp_mul_v(lb_v16u a, lb_v16u b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // hand-scheduled MAD chains (lb_fpmul_gfx950.h); bit-identical to fp_mul_body
+  fp x = fp_unpack(a), y = fp_unpack(b);
+  uint32_t o[12], top;
+  lbm_mont_mul(o, &top, x.v, y.v);
+  return fp_pack(fp_reduce_once(o, top));
+#else
   return fp_pack(fp_mul_body(fp_unpack(a), fp_unpack(b)));
+#endif
 }
 __host__ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
 #if defined(__HIP_DEVICE_COMPILE__)

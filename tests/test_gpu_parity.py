@@ -199,3 +199,15 @@ def test_pool_multithread_e2e_cases(engine):
         return r
 
     assert asyncio.run(main_thread()) is True
+
+
+def test_fp_mul_asm_matches_reference_body():
+    """The inline-asm Montgomery product (lb_fpmul_gfx950.h, used by every kernel) agrees with
+    the portable carry-save form fp_mul_body on 16.4M random and edge-case operands."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "ubench", "fpmul_asm")
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert json.loads(out.stdout.strip().splitlines()[-1])["mismatches"] == 0
