@@ -97,8 +97,29 @@ def build_ubench(force=False, verbose=True):
     return out
 
 
+NAPI = os.path.join(ROOT, "lodestar_amd", "napi", "lodestar_bls.node")
+
+
+def build_napi(force=False, verbose=True):
+    """N-API addon (plain C against the system node_api.h) linked to liblodestar_bls.so."""
+    src = os.path.join(ROOT, "lodestar_amd", "napi", "lb_napi.c")
+    hdr = "/usr/include/node/node_api.h"
+    if not os.path.exists(hdr):
+        return None
+    if not force and not _stale(NAPI, [src, LIB, os.path.join(INC, "lodestar_bls.h")]):
+        return NAPI
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-I/usr/include/node", "-I" + INC, src, "-o", NAPI + ".tmp",
+           "-L" + os.path.dirname(LIB), "-llodestar_bls", "-Wl,-rpath,$ORIGIN/.."]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(NAPI + ".tmp", NAPI)
+    return NAPI
+
+
 def build_all(force=False):
     build_lib(force)
+    build_napi(force)
     build_harness(force)
     build_cpu_pool(force)
     build_ubench(force)
