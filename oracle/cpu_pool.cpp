@@ -89,3 +89,71 @@ extern "C" int cpu_verify_jobs(uint32_t n_jobs, const uint32_t* job_off, const u
   for (auto& t : th) t.join();
   return 0;
 }
+
+// ---- multi-GPU protocol checker (CPU): the 576-byte partial of a shard and the product check,
+// the CPU counterparts of lb_batch_partial / lb_fp12_product_is_one (tests/test_distributed.py).
+extern "C" int cpu_partial(uint32_t n_jobs, const uint32_t* job_off, const uint32_t* pk_off, const uint8_t* pks,
+                           const uint8_t* msgs, const uint8_t* sigs, uint64_t seed, uint8_t* out576,
+                           int32_t* out_status) {
+  uint64_t rng = seed | 1;
+  fp12 f = fp12_one();
+  g2j S = jac_infinity<fp2>();
+  for (uint32_t j = 0; j < n_jobs; j++) {
+    uint32_t a = job_off[j], e = job_off[j + 1];
+    int st = a == e ? LB_EMPTY_SIGNATURE_SET : LB_OK;
+    std::vector<g1a> agg;
+    std::vector<g2a> sg;
+    std::vector<bool> sinf;
+    for (uint32_t i = a; i < e && st == LB_OK; i++) {
+      if (pk_off[i] == pk_off[i + 1]) { st = LB_EMPTY_AGGREGATE_ARRAY; break; }
+      g1j acc = jac_infinity<fp>();
+      for (uint32_t k = pk_off[i]; k < pk_off[i + 1] && st == LB_OK; k++) {
+        g1a p; bool inf;
+        st = g1_deserialize96(pks + (size_t)96 * k, p, inf);
+        if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+      }
+      g1a pa; jac_to_aff(pa, acc);
+      agg.push_back(jac_is_inf(acc) ? g1a{fp_zero(), fp_zero()} : pa);
+      if (jac_is_inf(acc) && st == LB_OK) st = -1;  // marker: infinity, resolved after sig decode
+    }
+    int pk_inf = st == -1;
+    if (pk_inf) st = LB_OK;
+    for (uint32_t i = a; i < e && st == LB_OK; i++) {
+      g2a s; bool inf;
+      st = g2_decompress96(sigs + (size_t)96 * i, s, inf);
+      if (st == LB_OK && !inf && !g2_in_subgroup(jac_from_aff(s))) st = LB_POINT_NOT_IN_GROUP;
+      sg.push_back(s); sinf.push_back(inf);
+    }
+    if (st == LB_OK && pk_inf) st = LB_PK_IS_INFINITY;
+    out_status[j] = st == LB_OK ? 1 : -st;
+    if (st != LB_OK) continue;
+    for (uint32_t i = a; i < e; i++) {
+      rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+      uint64_t r = rng | 1;
+      g1a rp;
+      jac_to_aff(rp, jac_mul_u64(agg[i - a], r));
+      if (!sinf[i - a]) S = jac_add(S, jac_mul_u64(sg[i - a], r));
+      g2a h;
+      jac_to_aff(h, hash_to_g2(msgs + (size_t)32 * i));
+      f = fp12_mul(f, miller_loop(rp, h));
+    }
+  }
+  if (!jac_is_inf(S)) {
+    g2a sa;
+    jac_to_aff(sa, S);
+    g1a ng1{fp_load(LB_G1X), fp_load(LB_G1NEGY)};
+    f = fp12_mul(f, miller_loop(ng1, sa));
+  }
+  fp12_to_be576(out576, f);
+  return 0;
+}
+
+extern "C" int cpu_product_is_one(const uint8_t* parts, uint32_t n) {
+  fp12 acc = fp12_one();
+  for (uint32_t i = 0; i < n; i++) {
+    fp12 f;
+    if (!fp12_from_be576(f, parts + (size_t)576 * i)) return 0;
+    acc = fp12_mul(acc, f);
+  }
+  return fp12_is_one(final_exponentiation(acc)) ? 1 : 0;
+}

@@ -1,0 +1,101 @@
+"""World-size-2 gloo run of the multi-GPU exchange protocol (lodestar_amd/distributed.py) on CPU,
+with the CPU counterparts of lb_batch_partial / lb_fp12_product_is_one (oracle/cpu_pool.cpp)."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT, load_json
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _jobs(bad_case=None):
+    from lodestar_amd.engine import SetInput
+    names = ["single_valid_0", "two_valid", "aggregate_valid", "aggregate_duplicate_keys", "k4_like_batch",
+             "mixed_valid_with_aggregate"]
+    if bad_case:
+        names.insert(3, bad_case)
+    cases = {c["name"]: c for c in load_json("jobs.json")["cases"]}
+    return [[SetInput([bytes.fromhex(p) for p in s["pubkeys"]], bytes.fromhex(s["signing_root"]),
+                      bytes.fromhex(s["signature"])) for s in cases[n]["sets"]] for n in names], \
+        [cases[n]["expected"] for n in names]
+
+
+def _worker(rank, world, port, bad_case, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from lodestar_amd.distributed import shard_jobs, verify_sharded
+    from lodestar_amd.engine import pack_jobs
+    from oracle.cpu_pool import _lib, run_jobs
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    jobs, _ = _jobs(bad_case)
+    lo, hi = shard_jobs(len(jobs), world, rank)
+    packed = pack_jobs(jobs[lo:hi])
+    lib = _lib()
+    P = lambda a, t: np.ascontiguousarray(a).ctypes.data_as(ctypes.POINTER(t))  # noqa: E731
+
+    def partial():
+        buf = (ctypes.c_uint8 * 576)()
+        st = np.zeros(packed.n_jobs, dtype=np.int32)
+        lib.cpu_partial(packed.n_jobs, P(packed.job_off, ctypes.c_uint32), P(packed.pk_off, ctypes.c_uint32),
+                        P(packed.pubkeys, ctypes.c_uint8), P(packed.msgs, ctypes.c_uint8),
+                        P(packed.sigs, ctypes.c_uint8), ctypes.c_uint64(0x1234 + rank),
+                        ctypes.cast(buf, ctypes.POINTER(ctypes.c_uint8)), P(st, ctypes.c_int32))
+        return bytes(buf), list(st)
+
+    def product(parts):
+        b = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+        return bool(lib.cpu_product_is_one(P(b, ctypes.c_uint8), len(parts)))
+
+    def local():
+        return list(run_jobs(packed, 0, packed.n_jobs, 2)[0])
+
+    codes, ok = verify_sharded(partial, product, local)
+    out.put((rank, lo, codes, ok))
+    dist.destroy_process_group()
+
+
+def _run(bad_case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, bad_case, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    codes = [c for _, _, cs, _ in res for c in cs]
+    return codes, [ok for *_, ok in res]
+
+
+def _expected_codes(exp):
+    from lodestar_amd import _native as N
+    names = {N.error_name(c): c for c in range(1, 13)}
+    return [(1 if e else 0) if isinstance(e, bool) else -names[e] for e in exp]
+
+
+def test_gloo_two_ranks_all_valid():
+    codes, oks = _run(None)
+    assert oks == [True, True]
+    assert codes == [1] * len(codes)
+
+
+def test_gloo_two_ranks_invalid_job_localised():
+    codes, oks = _run("batch_one_wrong")
+    assert oks == [False, False]
+    _, exp = _jobs("batch_one_wrong")
+    assert codes == _expected_codes(exp)
