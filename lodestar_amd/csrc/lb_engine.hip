@@ -93,7 +93,7 @@ struct lb_engine {
   int device = 0;
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
-  hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr;
+  hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr;
   std::mutex mu;
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
@@ -187,6 +187,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_s, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_dec, hipEventDisableTiming);
   for (int i = 0; i < kStages; i++) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
@@ -210,6 +211,7 @@ void lb_engine_destroy(lb_engine* e) {
   hipEventDestroy(e->ev_g1);
   hipEventDestroy(e->ev_s);
   hipEventDestroy(e->ev_fork);
+  hipEventDestroy(e->ev_dec);
   hipStreamSynchronize(e->stream2);
   hipStreamDestroy(e->stream2);
   hipStreamDestroy(e->stream);
@@ -354,12 +356,6 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   if (n) {
     // ---- s2: signatures, pubkeys, r*PK
     {
-      stage_scope sc(e, ST_DECODE, s2);
-      hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
-                         b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
-                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
-    }
-    {
       stage_scope sc(e, ST_PK_CHUNKS, s2);
       if (nc)
         hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
@@ -372,6 +368,14 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
     }
     LB_HIP(hipEventRecord(e->ev_g1, s2));
+    // signatures: decoded while s1 hashes and runs the Miller loops
+    {
+      stage_scope sc(e, ST_DECODE, s2);
+      hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
+                         b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
+                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+    }
+    LB_HIP(hipEventRecord(e->ev_dec, s2));
     // ---- s1: hash_to_G2
     {
       stage_scope sc(e, ST_HASH_MAP, s1);
@@ -395,11 +399,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     {
       stage_scope sc(e, ST_MILLER, s1);
       hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rpk.as<uint32_t>(),
-                         e->h_aff.as<uint32_t>(), e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(),
-                         e->ml.as<uint32_t>());
+                         e->h_aff.as<uint32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>());
     }
   } else {
     LB_HIP(hipEventRecord(e->ev_g1, s2));
+    LB_HIP(hipEventRecord(e->ev_dec, s2));
   }
   // ---- s2: S tree and ML(-G1, S_root)
   {
@@ -418,7 +422,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, m, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
   }
   LB_HIP(hipEventRecord(e->ev_s, s2));
-  // ---- s1: P tree
+  // ---- s1: P tree (job statuses need the signature decode from s2: recorded as ev_g1 below)
+  LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
   {
     stage_scope sc(e, ST_LEAVES_P, s1);
     hipLaunchKernelGGL(k_job_leaves_P, dim3(nblk(m)), dim3(LB_TPB), 0, s1, nj, n, m, b->d_job_off.as<uint32_t>(),

@@ -18,6 +18,9 @@
 #include "lb_pairing.h"
 
 #define LB_TPB 64  // one wave per workgroup: spreads few-thousand-item batches over all 256 CUs
+#ifndef LB_MINW
+#define LB_MINW 1  // min waves per SIMD (2 caps registers at 256 but spills: measured slower)
+#endif
 
 template <class T>
 __device__ __forceinline__ T soa_ld(const uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
@@ -59,7 +62,7 @@ __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + 
 
 // ---------------------------------------------------------------- signatures
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
-__global__ void __launch_bounds__(LB_TPB) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                         const uint32_t* __restrict__ sig_sizes,
                                                         uint32_t* __restrict__ sig_aff,
                                                         uint32_t* __restrict__ sig_inf,
@@ -86,7 +89,7 @@ __global__ void __launch_bounds__(LB_TPB) k_decode_sigs(uint32_t n, const uint8_
 
 // ---------------------------------------------------------------- hash_to_G2
 // thread t: set t % n, field element u_{t / n}; output Jacobian points q[2n]
-__global__ void __launch_bounds__(LB_TPB) k_hash_map(uint32_t n, const uint8_t* __restrict__ msgs,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const uint8_t* __restrict__ msgs,
                                                      uint32_t* __restrict__ q) {
   uint32_t t = lb_tid();
   if (t >= 2 * n) return;
@@ -102,7 +105,7 @@ __global__ void __launch_bounds__(LB_TPB) k_hash_map(uint32_t n, const uint8_t* 
   soa_st(q, 2 * n, t, p);
 }
 
-__global__ void __launch_bounds__(LB_TPB) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
                                                         uint32_t* __restrict__ h_aff) {
   uint32_t i = lb_tid();
   if (i >= n) return;
@@ -119,7 +122,7 @@ __global__ void __launch_bounds__(LB_TPB) k_hash_finish(uint32_t n, const uint32
 // keys so a 512-key sync aggregate costs one chunk's latency plus a short combine instead of
 // 512 serial additions on one lane; chunk c covers pubkeys [chunk_lo[c], chunk_lo[c+1]) of one set.
 #define LB_PK_CHUNK 16
-__global__ void __launch_bounds__(LB_TPB) k_pk_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                       const uint8_t* __restrict__ pks, uint32_t* __restrict__ chunk_acc,
                                                       int32_t* __restrict__ chunk_status) {
   uint32_t c = lb_tid();
@@ -141,7 +144,7 @@ __global__ void __launch_bounds__(LB_TPB) k_pk_chunks(uint32_t nc, const uint32_
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
 // r * PK for the Miller loop (critical path; the G2 side r * sig is k_sig_blind, off it).
-__global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
                                                      const uint32_t* __restrict__ chunk_acc,
                                                      const int32_t* __restrict__ chunk_status,
                                                      const uint32_t* __restrict__ pk_off,
@@ -173,7 +176,7 @@ __global__ void __launch_bounds__(LB_TPB) k_pk_blind(uint32_t n, uint32_t nc, co
 }
 
 // r * sig (Jacobian G2) for the aggregate-signature side of the batch equation
-__global__ void __launch_bounds__(LB_TPB) k_sig_blind(uint32_t n, const uint64_t* __restrict__ scalars,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_blind(uint32_t n, const uint64_t* __restrict__ scalars,
                                                       const uint32_t* __restrict__ sig_aff,
                                                       const uint32_t* __restrict__ sig_inf,
                                                       const int32_t* __restrict__ sig_status,
@@ -186,15 +189,16 @@ __global__ void __launch_bounds__(LB_TPB) k_sig_blind(uint32_t n, const uint64_t
 }
 
 // ---------------------------------------------------------------- Miller loops
-__global__ void __launch_bounds__(LB_TPB) k_miller(uint32_t n, const uint32_t* __restrict__ rpk_aff,
+// Needs only r*PK and H(m): signature decoding runs concurrently on the other stream, and a
+// set whose signature turns out malformed is dropped at the job leaves.
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const uint32_t* __restrict__ rpk_aff,
                                                    const uint32_t* __restrict__ h_aff,
-                                                   const int32_t* __restrict__ sig_status,
                                                    const int32_t* __restrict__ pk_status,
                                                    uint32_t* __restrict__ ml) {
   uint32_t i = lb_tid();
   if (i >= n) return;
   fp12 f = fp12_one();
-  if (sig_status[i] == LB_OK && pk_status[i] == LB_OK) {
+  if (pk_status[i] == LB_OK) {
     g1a p = soa_ld<g1a>(rpk_aff, n, i);
     g2a h = soa_ld<g2a>(h_aff, n, i);
     f = miller_loop(p, h);
@@ -218,7 +222,7 @@ __device__ __forceinline__ int job_status_of(uint32_t a, uint32_t e, const int32
 }
 
 // P_j = prod ML_i over the job's sets (identity for a rejecting job) -> treeP leaf m + j
-__global__ void __launch_bounds__(LB_TPB) k_job_leaves_P(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_job_leaves_P(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
                                                          const uint32_t* __restrict__ job_off,
                                                          const int32_t* __restrict__ sig_status,
                                                          const int32_t* __restrict__ pk_status,
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(LB_TPB) k_job_leaves_P(uint32_t n_jobs, uint32
 }
 
 // S_j = sum r_i sig_i over the job's sets (identity for a rejecting job) -> treeS leaf m + j
-__global__ void __launch_bounds__(LB_TPB) k_job_leaves_S(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_job_leaves_S(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
                                                          const uint32_t* __restrict__ job_off,
                                                          const int32_t* __restrict__ sig_status,
                                                          const int32_t* __restrict__ pk_status,
@@ -269,7 +273,7 @@ __global__ void __launch_bounds__(64) k_tree_up_P(uint32_t m, uint32_t lo, uint3
 }
 
 // G2 sum tree, one level, one lane per node (Jacobian additions)
-__global__ void __launch_bounds__(LB_TPB) k_tree_up_S(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeS) {
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_tree_up_S(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeS) {
   uint32_t t = lb_tid();
   if (t >= lo) return;
   uint32_t i = lo + t;
@@ -366,7 +370,7 @@ __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t
 }
 
 // ---------------------------------------------------------------- pubkey aggregation only
-__global__ void __launch_bounds__(LB_TPB) k_aggregate(uint32_t n, const uint32_t* __restrict__ pk_off,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_aggregate(uint32_t n, const uint32_t* __restrict__ pk_off,
                                                       const uint8_t* __restrict__ pks, uint8_t* __restrict__ out96,
                                                       int32_t* __restrict__ status) {
   uint32_t i = lb_tid();
@@ -394,7 +398,7 @@ __global__ void __launch_bounds__(LB_TPB) k_aggregate(uint32_t n, const uint32_t
 // 48-byte compressed pubkeys -> 96-byte uncompressed (the pubkey cache's one-time
 // deserialisation, state-transition/src/cache/pubkeyCache.ts:56-77).  validate = subgroup
 // + infinity check (PublicKey.keyValidate).
-__global__ void __launch_bounds__(LB_TPB) k_g1_decompress(uint32_t n, const uint8_t* __restrict__ in48,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_decompress(uint32_t n, const uint8_t* __restrict__ in48,
                                                           uint8_t* __restrict__ out96, int32_t* __restrict__ status,
                                                           int32_t validate) {
   uint32_t i = lb_tid();
@@ -422,7 +426,7 @@ __global__ void __launch_bounds__(LB_TPB) k_g1_decompress(uint32_t n, const uint
 
 // ---------------------------------------------------------------- synthetic data (bench/tests)
 // sk (32-byte big-endian, < r) -> 48-byte compressed and 96-byte uncompressed pubkey
-__global__ void __launch_bounds__(LB_TPB) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks,
                                                      uint8_t* __restrict__ out48, uint8_t* __restrict__ out96) {
   uint32_t i = lb_tid();
   if (i >= n) return;
@@ -444,7 +448,7 @@ __global__ void __launch_bounds__(LB_TPB) k_sk_to_pk(uint32_t n, const uint8_t* 
 }
 
 // sig = sk * H(m), 96-byte compressed
-__global__ void __launch_bounds__(LB_TPB) k_sign(uint32_t n, const uint8_t* __restrict__ sks,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sign(uint32_t n, const uint8_t* __restrict__ sks,
                                                  const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
   uint32_t i = lb_tid();
   if (i >= n) return;
