@@ -105,9 +105,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): LB_BENCH_BACKEND=gloo + LB_BENCH_DEVICE=0 run N ranks
+    # on one GPU with CPU-side collectives
+    backend = os.environ.get("LB_BENCH_BACKEND", "nccl")
+    if os.environ.get("LB_BENCH_DEVICE") is not None:
+        local = int(os.environ["LB_BENCH_DEVICE"])
+    coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from lodestar_amd.engine import Engine
     from lodestar_amd import workloads as W
@@ -131,7 +140,7 @@ def main():
             # 576-byte partials over RCCL, one final exponentiation of their product (distributed.py)
             from lodestar_amd.distributed import verify_sharded
             codes, _ = verify_sharded(batch.partial, eng.product_is_one, batch.verify,
-                                      device=torch.device("cuda", local))
+                                      device=coll_dev if coll_dev.type == "cuda" else None)
         else:
             codes = batch.verify()
         return codes
@@ -177,11 +186,11 @@ def main():
         el = time.perf_counter() - t1
         for r in res:
             assert np.array_equal(np.asarray(r) == 1, wl.expected == 1), "verification results differ"
-    el_t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    el_t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
-    es_t = torch.tensor([el_single], dtype=torch.float64, device="cuda")
+    es_t = torch.tensor([el_single], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(es_t, op=dist.ReduceOp.MAX)
     value_single = n_sets * world * a.steps / float(es_t.item())

@@ -434,17 +434,18 @@ LB_HD fp6 fp6_sub(const fp6& a, const fp6& b) { return fp6{fp2_sub(a.c0, b.c0), 
 LB_HD fp6 fp6_neg(const fp6& a) { return fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 LB_HD fp6 fp6_mul_v(const fp6& a) { return fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
-LB_NI void fp6_mul_p(fp6* r, const fp6* pa, const fp6* pb) {
-  const fp6& a = *pa;
-  const fp6& b = *pb;
+// Inline body (the Miller loop kernel keeps its Fp12 state in registers); fp6_mul_p is the
+// out-of-line entry everything else calls.
+LB_HD fp6 fp6_mul_inl(const fp6& a, const fp6& b) {
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
   fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
   fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
   fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
-  *r = fp6{c0, c1, c2};
+  return fp6{c0, c1, c2};
 }
+LB_NI void fp6_mul_p(fp6* r, const fp6* pa, const fp6* pb) { *r = fp6_mul_inl(*pa, *pb); }
 LB_HD fp6 fp6_mul(const fp6& a, const fp6& b) {
   fp6 r;
   fp6_mul_p(&r, &a, &b);
@@ -498,14 +499,14 @@ LB_HD fp12 fp12_mul(const fp12& a, const fp12& b) {
   return r;
 }
 
-LB_NI void fp12_sqr_p(fp12* r, const fp12* pa) {
+LB_HD fp12 fp12_sqr_inl(const fp12& a) {
   // complex squaring: (a0 + a1 w)^2 = a0^2 + v a1^2 + 2 a0 a1 w
-  const fp12& a = *pa;
-  fp6 t = fp6_mul(a.c0, a.c1);
-  fp6 c0 = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6 t = fp6_mul_inl(a.c0, a.c1);
+  fp6 c0 = fp6_mul_inl(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   c0 = fp6_sub(fp6_sub(c0, t), fp6_mul_v(t));
-  *r = fp12{c0, fp6_add(t, t)};
+  return fp12{c0, fp6_add(t, t)};
 }
+LB_NI void fp12_sqr_p(fp12* r, const fp12* pa) { *r = fp12_sqr_inl(*pa); }
 LB_HD fp12 fp12_sqr(const fp12& a) {
   fp12 r;
   fp12_sqr_p(&r, &a);
@@ -513,14 +514,15 @@ LB_HD fp12 fp12_sqr(const fp12& a) {
 }
 
 // multiply by a Miller-loop line  l = (l0 + l2 v) + (l3 v) w   (w-basis: l0 w^0 + l2 w^2 + l3 w^3)
-LB_NI void fp12_mul_line_p(fp12* r, const fp12* pa, const fp2* pl0, const fp2* pl2, const fp2* pl3) {
-  const fp12& a = *pa;
-  const fp2 &l0 = *pl0, &l2 = *pl2, &l3 = *pl3;
+LB_HD fp12 fp12_mul_line_inl(const fp12& a, const fp2& l0, const fp2& l2, const fp2& l3) {
   fp6 t0 = fp6_mul_01(a.c0, l0, l2);
   fp6 t1 = fp6_mul_1(a.c1, l3);
   fp6 c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(a.c0, a.c1), l0, fp2_add(l2, l3)), t0), t1);
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
-  *r = fp12{c0, c1};
+  return fp12{c0, c1};
+}
+LB_NI void fp12_mul_line_p(fp12* r, const fp12* pa, const fp2* pl0, const fp2* pl2, const fp2* pl3) {
+  *r = fp12_mul_line_inl(*pa, *pl0, *pl2, *pl3);
 }
 LB_HD fp12 fp12_mul_line(const fp12& a, const fp2& l0, const fp2& l2, const fp2& l3) {
   fp12 r;

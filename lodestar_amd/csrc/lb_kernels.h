@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const ui
   if (pk_status[i] == LB_OK) {
     g1a p = soa_ld<g1a>(rpk_aff, n, i);
     g2a h = soa_ld<g2a>(h_aff, n, i);
-    f = miller_loop(p, h);
+    f = miller_loop_inl(p, h);
   }
   soa_st(ml, n, i, f);
 }

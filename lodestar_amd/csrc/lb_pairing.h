@@ -11,7 +11,7 @@
 #include "lb_curve.h"
 
 // doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P
-LB_NI void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
   const fp2 b3 = fp2_load(LB_B2_3);  // 3 b'
   fp2 X = T.x, Y = T.y, Z = T.z;
   fp2 A = fp2_mul(X, Y);             // XY (halved below)
@@ -36,7 +36,7 @@ LB_NI void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp&
 }
 
 // addition step T <- T + Q (Q affine), line through T and Q at P
-LB_NI void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
+LB_HD void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
   fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
   // line: (theta xQ - lam yQ) + (-theta xP) w^2 + (lam yP) w^3
@@ -74,6 +74,33 @@ LB_NI fp12 miller_loop(g1a P, g2a Q) {
     if ((LB_X_ABS >> i) & 1ull) {
       miller_add(T, Q, l0, l2, l3, P.x, P.y);
       f = fp12_mul_line(f, l0, l2, l3);
+    }
+  }
+  return fp12_conj(f);
+}
+
+// Same loop with the Fp12 squaring / line multiplication / point steps inlined, so f, T and
+// the line values stay in registers (only fp_mul is a call).  The pointer-argument versions
+// cost ~8 GB of scratch traffic per 19k-pair launch (profiles/r1_pmc_*).
+LB_HD fp12 miller_loop_inl(const g1a& P, const g2a& Q) {
+  g2j T;
+  T.x = Q.x;
+  T.y = Q.y;
+  T.z = fp2_one();
+  fp2 l0, l2, l3;
+  fp12 f = fp12_one();
+  bool first = true;
+  for (int i = 62; i >= 0; i--) {
+    if (!first) f = fp12_sqr_inl(f);
+    miller_dbl(T, l0, l2, l3, P.x, P.y);
+    if (first) {
+      f = fp12_one();
+      first = false;
+    }
+    f = fp12_mul_line_inl(f, l0, l2, l3);
+    if ((LB_X_ABS >> i) & 1ull) {
+      miller_add(T, Q, l0, l2, l3, P.x, P.y);
+      f = fp12_mul_line_inl(f, l0, l2, l3);
     }
   }
   return fp12_conj(f);
