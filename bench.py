@@ -35,6 +35,7 @@ def parse():
                     help="batches in flight per GPU: independent engines (own streams + workspaces) driven by "
                          "one host thread each, like the reference pool's concurrent workers")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pubkey-bytes", action="store_true", help="ship 96-byte pubkeys instead of table indices")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     return ap.parse_args()
@@ -126,7 +127,14 @@ def main():
     t0 = time.time()
     wl = W.make(eng, a.workload, seed=W.SEED + rank)
     gen_s = time.time() - t0
-    batches = [e.upload(wl.packed) for e in engs]
+    # pubkeys as indices into each engine's resident table (the epoch cache's index2pubkey path);
+    # --pubkey-bytes ships 96-byte keys instead
+    if a.pubkey_bytes:
+        batches = [e.upload(W.PackedJobs(job_off=wl.packed.job_off, pk_off=wl.packed.pk_off,
+                                         pubkeys=wl.packed.pubkeys, msgs=wl.packed.msgs, sigs=wl.packed.sigs,
+                                         sig_sizes=None)) for e in engs]
+    else:
+        batches = [e.upload(W.indexed_for(e, wl)) for e in engs]
     batch = batches[0]
     n_sets, n_jobs = wl.packed.n_sets, wl.packed.n_jobs
 
@@ -215,7 +223,8 @@ def main():
             "config": {"workload": f"{a.workload}: gossip attestation flood, one slot per GPU" if a.workload == "c3"
                        else a.workload, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
                        "pubkeys_per_gpu": int(wl.packed.pk_off[-1]), "parallelism": f"dp{world} (sets sharded)",
-                       "exchange": bool(a.exchange), "inflight": a.inflight},
+                       "exchange": bool(a.exchange), "inflight": a.inflight,
+                       "pubkeys": "96-byte keys per set" if a.pubkey_bytes else "indices into the GPU-resident table"},
             "value_one_batch_in_flight": round(value_single, 1),
             "roofline": roof, "cpu_baseline": cpu, "gen_s": round(gen_s, 2),
         }), flush=True)

@@ -140,6 +140,28 @@ int32_t lb_sk_to_pk(lb_engine* e, uint32_t n, const uint8_t* sks32, uint8_t* out
 int32_t lb_sign(lb_engine* e, uint32_t n, const uint8_t* sks32, const uint8_t* msgs32, uint8_t* out96);
 
 /*
+ * GPU-resident pubkey table (the epoch cache's index2pubkey,
+ * state-transition/src/cache/pubkeyCache.ts:56-77, epochContext.ts:704).  Keys are decoded once
+ * (48-byte compressed or 96-byte uncompressed, key_size says which) into affine Montgomery form in
+ * HBM; out_status[n] gets LB_OK or the decode error (validate != 0 adds the infinity + subgroup
+ * checks of PublicKey.keyValidate).  Appending extends the table (new validators); the table
+ * belongs to the engine.
+ */
+int32_t lb_pubkey_table_append(lb_engine* e, uint32_t n, const uint8_t* keys, uint32_t key_size, int32_t validate,
+                               int32_t* out_status, uint32_t* out_first_index);
+uint32_t lb_pubkey_table_size(const lb_engine* e);
+
+/*
+ * Like lb_batch_create, but set i aggregates table entries pk_indices[set_pk_offsets[i] ..
+ * set_pk_offsets[i+1]) instead of carrying pubkey bytes (4 bytes per key on the bus instead of 96).
+ * An index beyond the table makes that set's job reject with LB_ERR_ARGUMENT.
+ */
+int32_t lb_batch_create_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                                const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
+                                const uint8_t* signing_roots, const uint8_t* signatures,
+                                const uint32_t* sig_sizes, lb_batch** out);
+
+/*
  * Per-stage device timings of the last lb_batch_verify / lb_batch_partial on this engine,
  * measured with HIP events on the engine's stream.  names[i] / ms[i] for i < *n (max cap).
  */

@@ -57,6 +57,11 @@ SIGNATURES = {
     "lb_g1_decompress": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _i32p, ctypes.c_int32]),
     "lb_sk_to_pk": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),
     "lb_sign": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),
+    "lb_pubkey_table_append": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_int32, _i32p,
+                                                _u32p]),
+    "lb_pubkey_table_size": (ctypes.c_uint32, [_vp]),
+    "lb_batch_create_indexed": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u32p, _u32p, _u8p, _u8p, _u32p,
+                                                 ctypes.POINTER(_vp)]),
     "lb_engine_set_profiling": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "lb_engine_last_profile": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_char_p),
                                                 ctypes.POINTER(ctypes.c_float), ctypes.c_int32, _i32p]),

@@ -74,6 +74,7 @@ struct lb_batch {
   uint32_t n_jobs = 0, n_sets = 0, n_pks = 0;
   std::vector<uint32_t> job_off;  // host copy (bisection bookkeeping)
   uint32_t n_chunks = 0;           // pubkey aggregation chunks (k_pk_chunks)
+  bool indexed = false;            // pubkeys are indices into the engine's resident table
   dbuf d_job_off, d_pk_off, d_pks, d_msgs, d_sigs, d_sig_sizes, d_set_chunk_off, d_chunk_lo;
   bool has_sizes = false;
   int device = 0;
@@ -99,6 +100,9 @@ struct lb_engine {
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
       nodes, verdict, parts, ok, chunk_acc, chunk_status, fS;
   std::vector<uint64_t> h_scalars;
+  // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
+  dbuf table, table_flag;
+  uint32_t table_n = 0, table_cap = 0;
   // profiling
   bool profiling = false;
   hipEvent_t ev0[kStages] = {}, ev1[kStages] = {};
@@ -202,7 +206,7 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamSynchronize(e->stream);
   dbuf* bufs[] = {&e->scalars, &e->sig_aff, &e->sig_inf, &e->sig_status, &e->q, &e->h_aff, &e->rpk, &e->rsig,
                   &e->pk_status, &e->ml, &e->treeP, &e->treeS, &e->job_status, &e->nodes, &e->verdict, &e->parts,
-                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS};
+                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->table_flag};
   for (dbuf* b : bufs) b->release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
@@ -235,9 +239,11 @@ int32_t lb_engine_last_profile(lb_engine* e, const char** names, float* ms, int3
   return LB_OK;
 }
 
-int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets,
-                        const uint8_t* pubkeys, const uint8_t* signing_roots, const uint8_t* signatures,
-                        const uint32_t* sig_sizes, lb_batch** out) {
+}  // extern "C"
+
+static int32_t batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets,
+                            const uint8_t* pubkeys, const uint32_t* pk_indices, const uint8_t* signing_roots,
+                            const uint8_t* signatures, const uint32_t* sig_sizes, lb_batch** out) {
   if (!e || !out || !job_offsets || !set_pk_offsets) return LB_ERR_ARGUMENT;
   *out = nullptr;
   if (job_offsets[0] != 0) return LB_ERR_ARGUMENT;
@@ -248,7 +254,8 @@ int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offse
   for (uint32_t i = 0; i < n_sets; i++)
     if (set_pk_offsets[i + 1] < set_pk_offsets[i]) return LB_ERR_ARGUMENT;
   uint32_t n_pks = set_pk_offsets[n_sets];
-  if ((n_sets && (!signing_roots || !signatures)) || (n_pks && !pubkeys)) return LB_ERR_ARGUMENT;
+  const bool indexed = pk_indices != nullptr;
+  if ((n_sets && (!signing_roots || !signatures)) || (n_pks && !pubkeys && !indexed)) return LB_ERR_ARGUMENT;
   std::lock_guard<std::mutex> lk(e->mu);
   LB_HIP(hipSetDevice(e->device));
   lb_batch* b = new lb_batch();
@@ -277,7 +284,8 @@ int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offse
   if (r == hipSuccess) r = up(b->d_set_chunk_off, set_chunk_off.data(), set_chunk_off.size() * 4);
   if (r == hipSuccess) r = up(b->d_chunk_lo, chunk_lo.data(), chunk_lo.size() * 4);
   if (r == hipSuccess) r = up(b->d_pk_off, set_pk_offsets, (size_t)(n_sets + 1) * 4);
-  if (r == hipSuccess) r = up(b->d_pks, pubkeys, (size_t)n_pks * 96);
+  b->indexed = indexed;
+  if (r == hipSuccess) r = indexed ? up(b->d_pks, pk_indices, (size_t)n_pks * 4) : up(b->d_pks, pubkeys, (size_t)n_pks * 96);
   if (r == hipSuccess) r = up(b->d_msgs, signing_roots, (size_t)n_sets * 32);
   if (r == hipSuccess) r = up(b->d_sigs, signatures, (size_t)n_sets * 96);
   if (r == hipSuccess && sig_sizes) r = up(b->d_sig_sizes, sig_sizes, (size_t)n_sets * 4);
@@ -288,6 +296,81 @@ int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offse
     return LB_ERR_DEVICE;
   }
   *out = b;
+  return LB_OK;
+}
+
+extern "C" {
+
+int32_t lb_batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets,
+                        const uint8_t* pubkeys, const uint8_t* signing_roots, const uint8_t* signatures,
+                        const uint32_t* sig_sizes, lb_batch** out) {
+  return batch_create(e, n_jobs, job_offsets, set_pk_offsets, pubkeys, nullptr, signing_roots, signatures, sig_sizes,
+                      out);
+}
+
+int32_t lb_batch_create_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                                const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
+                                const uint8_t* signing_roots, const uint8_t* signatures, const uint32_t* sig_sizes,
+                                lb_batch** out) {
+  if (!pk_indices && set_pk_offsets && job_offsets) {
+    // no keys at all is only valid when every set is empty
+    return batch_create(e, n_jobs, job_offsets, set_pk_offsets, nullptr, reinterpret_cast<const uint32_t*>(""),
+                        signing_roots, signatures, sig_sizes, out);
+  }
+  return batch_create(e, n_jobs, job_offsets, set_pk_offsets, nullptr, pk_indices, signing_roots, signatures,
+                      sig_sizes, out);
+}
+
+uint32_t lb_pubkey_table_size(const lb_engine* e) { return e ? e->table_n : 0; }
+
+int32_t lb_pubkey_table_append(lb_engine* e, uint32_t n, const uint8_t* keys, uint32_t key_size, int32_t validate,
+                               int32_t* out_status, uint32_t* out_first_index) {
+  if (!e || (n && (!keys || !out_status)) || (key_size != 48 && key_size != 96)) return LB_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(e->mu);
+  LB_HIP(hipSetDevice(e->device));
+  const uint32_t first = e->table_n;
+  if (out_first_index) *out_first_index = first;
+  if (!n) return LB_OK;
+  const uint32_t need = first + n;
+  if (need > e->table_cap) {
+    // grow: SoA stride changes, so move word rows one by one
+    uint32_t cap = e->table_cap ? e->table_cap : 1024;
+    while (cap < need) cap *= 2;
+    dbuf nt, nf;
+    LB_HIP(nt.ensure((size_t)cap * sizeof(g1a)));
+    LB_HIP(nf.ensure((size_t)cap * 4));
+    const int words = (int)(sizeof(g1a) / 4);
+    for (int w = 0; w < words && first; w++)
+      LB_HIP(hipMemcpyAsync(nt.as<uint32_t>() + (size_t)w * cap, e->table.as<uint32_t>() + (size_t)w * e->table_cap,
+                            (size_t)first * 4, hipMemcpyDeviceToDevice, e->stream));
+    if (first)
+      LB_HIP(hipMemcpyAsync(nf.p, e->table_flag.p, (size_t)first * 4, hipMemcpyDeviceToDevice, e->stream));
+    LB_HIP(hipStreamSynchronize(e->stream));
+    e->table.release();
+    e->table_flag.release();
+    e->table = nt;
+    e->table_flag = nf;
+    e->table_cap = cap;
+  }
+  dbuf kin, st;
+  hipError_t r = kin.ensure((size_t)n * key_size);
+  if (r == hipSuccess) r = st.ensure((size_t)n * 4);
+  if (r == hipSuccess) r = hipMemcpyAsync(kin.p, keys, (size_t)n * key_size, hipMemcpyHostToDevice, e->stream);
+  if (r == hipSuccess) {
+    hipLaunchKernelGGL(k_table_fill, dim3(nblk(n)), dim3(LB_TPB), 0, e->stream, n, kin.as<uint8_t>(), key_size,
+                       validate, first, e->table.as<uint32_t>(), e->table_cap, e->table_flag.as<uint32_t>(),
+                       st.as<int32_t>());
+    r = hipGetLastError();
+  }
+  if (r == hipSuccess) r = hipMemcpyAsync(out_status, st.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream);
+  if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+  kin.release();
+  st.release();
+  if (r != hipSuccess) {
+    fprintf(stderr, "lodestar_bls: pubkey table append failed: %s\n", hipGetErrorString(r));
+    return LB_ERR_DEVICE;
+  }
+  e->table_n = need;
   return LB_OK;
 }
 
@@ -357,7 +440,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // ---- s2: signatures, pubkeys, r*PK
     {
       stage_scope sc(e, ST_PK_CHUNKS, s2);
-      if (nc)
+      if (nc && b->indexed)
+        hipLaunchKernelGGL(k_pk_chunks_idx, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
+                           b->d_pks.as<uint32_t>(), e->table.as<uint32_t>(), e->table_cap,
+                           e->table_flag.as<uint32_t>(), e->table_n, e->chunk_acc.as<uint32_t>(),
+                           e->chunk_status.as<int32_t>());
+      else if (nc)
         hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
                            b->d_pks.as<uint8_t>(), e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>());
     }

@@ -142,6 +142,74 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, cons
   chunk_status[c] = st;
 }
 
+// Same as k_pk_chunks over the resident pubkey table (affine Montgomery, g1a SoA with
+// table_cap elements).  table_flag[t] = (decode status << 1) | is_infinity.  idx = pk_indices.
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks_idx(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
+                                                          const uint32_t* __restrict__ idx,
+                                                          const uint32_t* __restrict__ table, uint32_t table_cap,
+                                                          const uint32_t* __restrict__ table_flag, uint32_t table_n,
+                                                          uint32_t* __restrict__ chunk_acc,
+                                                          int32_t* __restrict__ chunk_status) {
+  uint32_t c = lb_tid();
+  if (c >= nc) return;
+  uint32_t a = chunk_lo[c], e = chunk_lo[c + 1];
+  int st = LB_OK;
+  g1j acc = jac_infinity<fp>();
+  for (uint32_t k = a; k < e; k++) {
+    uint32_t t = idx[k];
+    if (t >= table_n) {
+      st = LB_ERR_ARGUMENT;
+      break;
+    }
+    const uint32_t fl = table_flag[t];
+    if (fl >> 1) {
+      st = (int)(fl >> 1);
+      break;
+    }
+    if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
+    acc = jac_add_aff(acc, soa_ld<g1a>(table, table_cap, t));
+  }
+  soa_st(chunk_acc, nc, c, acc);
+  chunk_status[c] = st;
+}
+
+// decode keys into the resident table (48 B compressed or 96 B uncompressed)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, const uint8_t* __restrict__ keys,
+                                                       uint32_t key_size, int32_t validate, uint32_t first,
+                                                       uint32_t* __restrict__ table, uint32_t table_cap,
+                                                       uint32_t* __restrict__ table_flag, int32_t* __restrict__ status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  g1a a;
+  bool inf = false;
+  int st;
+  if (key_size == 48) {
+    uint8_t b[48];
+    for (int k = 0; k < 48; k++) b[k] = keys[(size_t)48 * i + k];
+    st = g1_decompress48(b, a, inf);
+  } else {
+    uint8_t b[96];
+    for (int k = 0; k < 96; k++) b[k] = keys[(size_t)96 * i + k];
+    st = g1_deserialize96(b, a, inf);
+  }
+  if (st == LB_OK && validate) {
+    if (inf) {
+      st = LB_PK_IS_INFINITY;
+    } else {
+      const uint32_t rr[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                              0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+      if (!jac_is_inf(jac_mul_u256(a, rr))) st = LB_POINT_NOT_IN_GROUP;
+    }
+  }
+  if (st != LB_OK) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  }
+  soa_st(table, table_cap, first + i, a);
+  table_flag[first + i] = ((uint32_t)st << 1) | (inf ? 1u : 0u);
+  status[i] = st;
+}
+
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
 // r * PK for the Miller loop (critical path; the G2 side r * sig is k_sig_blind, off it).
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,

@@ -38,10 +38,11 @@ class SetInput:
 class PackedJobs:
     job_off: np.ndarray    # uint32 [n_jobs+1]
     pk_off: np.ndarray     # uint32 [n_sets+1]
-    pubkeys: np.ndarray    # uint8  [n_pks*96]
+    pubkeys: Optional[np.ndarray]    # uint8  [n_pks*96]  (None when pk_indices is used)
     msgs: np.ndarray       # uint8  [n_sets*32]
     sigs: np.ndarray       # uint8  [n_sets*96]
     sig_sizes: Optional[np.ndarray]  # uint32 [n_sets] or None
+    pk_indices: Optional[np.ndarray] = None  # uint32 [n_pks]: indices into the engine's pubkey table
 
     @property
     def n_jobs(self):
@@ -102,10 +103,19 @@ class Batch:
         self.engine = engine
         self.packed = packed
         h = ctypes.c_void_p()
-        _check(engine.lib.lb_batch_create(
-            engine.h, packed.n_jobs, _p(packed.job_off, ctypes.c_uint32), _p(packed.pk_off, ctypes.c_uint32),
-            _p(packed.pubkeys, ctypes.c_uint8), _p(packed.msgs, ctypes.c_uint8), _p(packed.sigs, ctypes.c_uint8),
-            _p(packed.sig_sizes, ctypes.c_uint32), ctypes.byref(h)))
+        if packed.pk_indices is not None:
+            idx = np.ascontiguousarray(packed.pk_indices, dtype=np.uint32)
+            if idx.size == 0:
+                idx = np.zeros(1, dtype=np.uint32)
+            _check(engine.lib.lb_batch_create_indexed(
+                engine.h, packed.n_jobs, _p(packed.job_off, ctypes.c_uint32), _p(packed.pk_off, ctypes.c_uint32),
+                _p(idx, ctypes.c_uint32), _p(packed.msgs, ctypes.c_uint8), _p(packed.sigs, ctypes.c_uint8),
+                _p(packed.sig_sizes, ctypes.c_uint32), ctypes.byref(h)))
+        else:
+            _check(engine.lib.lb_batch_create(
+                engine.h, packed.n_jobs, _p(packed.job_off, ctypes.c_uint32), _p(packed.pk_off, ctypes.c_uint32),
+                _p(packed.pubkeys, ctypes.c_uint8), _p(packed.msgs, ctypes.c_uint8), _p(packed.sigs, ctypes.c_uint8),
+                _p(packed.sig_sizes, ctypes.c_uint32), ctypes.byref(h)))
         self.h = h
 
     @property
@@ -178,6 +188,18 @@ class Engine:
         finally:
             b.free()
 
+    def verify_jobs_indexed(self, jobs, indices, scalars: Optional[np.ndarray] = None) -> List[int]:
+        """Jobs whose pubkeys are table indices: indices[j][s] = list of table indices of set s."""
+        packed = pack_jobs([[SetInput([bytes(96)] * len(ix), s.signing_root, s.signature)
+                             for s, ix in zip(job, jix)] for job, jix in zip(jobs, indices)])
+        packed.pubkeys = None
+        packed.pk_indices = np.asarray([i for jix in indices for ix in jix for i in ix], dtype=np.uint32)
+        b = Batch(self, packed)
+        try:
+            return [int(x) for x in b.verify(scalars)]
+        finally:
+            b.free()
+
     def product_is_one(self, partials: Sequence[bytes]) -> bool:
         buf = np.frombuffer(b"".join(partials), dtype=np.uint8).copy() if partials else np.zeros(1, np.uint8)
         ok = ctypes.c_int32(0)
@@ -185,6 +207,25 @@ class Engine:
         return bool(ok.value)
 
     # ---------------------------------------------------------------- pubkeys
+    def pubkey_table_append(self, keys: Sequence[bytes], validate: bool = False) -> Tuple[int, List[int]]:
+        """Decode keys (all 48-byte compressed or all 96-byte uncompressed) into the resident table.
+        Returns (index of the first appended key, per-key status)."""
+        n = len(keys)
+        if n == 0:
+            return self.pubkey_table_size(), []
+        size = len(keys[0])
+        if any(len(k) != size for k in keys) or size not in (48, 96):
+            raise ValueError("keys must all be 48 or all be 96 bytes")
+        buf = np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8).copy()
+        st = np.zeros(n, dtype=np.int32)
+        first = ctypes.c_uint32(0)
+        _check(self.lib.lb_pubkey_table_append(self.h, n, _p(buf, ctypes.c_uint8), size, 1 if validate else 0,
+                                               _p(st, ctypes.c_int32), ctypes.byref(first)))
+        return int(first.value), [int(x) for x in st]
+
+    def pubkey_table_size(self) -> int:
+        return int(self.lib.lb_pubkey_table_size(self.h))
+
     def aggregate_pubkeys(self, sets_pubkeys: Sequence[Sequence[bytes]]) -> Tuple[List[bytes], List[int]]:
         off = [0]
         flat = []

@@ -54,12 +54,13 @@ class PublicKey:
     """A G1 public key held as its 96-byte uncompressed encoding (what the reference's main
     thread sends to workers: getAggregatedPubkey(s).toBytes(uncompressed))."""
 
-    __slots__ = ("raw",)
+    __slots__ = ("raw", "index")
 
-    def __init__(self, raw96: bytes):
+    def __init__(self, raw96: bytes, index: Optional[int] = None):
         if len(raw96) != 96:
             raise ValueError("PublicKey expects 96-byte uncompressed bytes")
         self.raw = bytes(raw96)
+        self.index = index  # position in the engine's resident pubkey table, if registered
 
     @staticmethod
     def many_from_compressed(engine: Engine, pks48: Sequence[bytes], validate: bool = False) -> List["PublicKey"]:
@@ -103,6 +104,14 @@ class VerifySignatureOpts:
     verify_on_main_thread: bool = False
 
 
+def _pk_list(s: ISignatureSet) -> List[PublicKey]:
+    if s.type == SignatureSetType.single:
+        return [s.pubkey]
+    if s.type == SignatureSetType.aggregate:
+        return list(s.pubkeys)
+    raise ValueError("Unknown signature set type")
+
+
 def _to_input(s: ISignatureSet) -> SetInput:
     if s.type == SignatureSetType.single:
         pks = [s.pubkey.raw]
@@ -122,6 +131,7 @@ def _result(code: int) -> bool:
 @dataclass
 class _Job:
     sets: List[SetInput]
+    idx: Optional[List[List[int]]]  # per set: pubkey table indices (None if any key is unregistered)
     opts: VerifySignatureOpts
     future: asyncio.Future
     loop: asyncio.AbstractEventLoop
@@ -161,13 +171,20 @@ class BlsGpuVerifier:
         if self._closed:
             raise QueueError("QUEUE_ABORTED")
         inputs = [_to_input(s) for s in sets]
+        idx = []
+        for s in sets:
+            pks = _pk_list(s)
+            idx.append([p.index for p in pks] if all(p.index is not None for p in pks) else None)
         if opts.verify_on_main_thread and not self.bls_verify_all_multi_thread:
             # synchronous, blocks the caller like the reference (multithread/index.ts:138-151)
             return _result(self.engine.verify_jobs([inputs])[0])
         loop = asyncio.get_running_loop()
         futs = []
-        for chunk in chunkify_maximize_chunk_size(inputs, MAX_SIGNATURE_SETS_PER_JOB):
-            job = _Job(sets=chunk, opts=opts, future=loop.create_future(), loop=loop)
+        chunks = chunkify_maximize_chunk_size(list(range(len(inputs))), MAX_SIGNATURE_SETS_PER_JOB)
+        for chunk in chunks:
+            cidx = [idx[i] for i in chunk]
+            job = _Job(sets=[inputs[i] for i in chunk], idx=None if (not cidx or any(x is None for x in cidx)) else cidx,
+                       opts=opts, future=loop.create_future(), loop=loop)
             futs.append(job.future)
             self._queue(job)
         results = await asyncio.gather(*futs)
@@ -187,6 +204,17 @@ class BlsGpuVerifier:
         await asyncio.get_running_loop().run_in_executor(None, self._runner.join)
         if self._own_engine:
             self.engine.close()
+
+    def register_pubkeys(self, pks: Sequence[bytes], validate: bool = False) -> List[PublicKey]:
+        """Load keys (48-byte compressed or 96-byte uncompressed) into the GPU-resident table once,
+        like the epoch cache's index2pubkey (pubkeyCache.ts:56-77); returned PublicKeys carry their
+        table index, so sets built from them ship 4-byte indices instead of 96-byte keys."""
+        first, st = self.engine.pubkey_table_append(list(pks), validate)
+        for s in st:
+            if s:
+                raise BlsError(s)
+        raws = list(pks) if len(pks) and len(pks[0]) == 96 else self.engine.g1_decompress(list(pks))[0]
+        return [PublicKey(r, first + k) for k, r in enumerate(raws)]
 
     # ---------------------------------------------------------------- queueing policy
     def _queue(self, job: _Job):
@@ -221,7 +249,10 @@ class BlsGpuVerifier:
                     return
                 jobs, self._jobs = self._jobs, []
             try:
-                codes = self.engine.verify_jobs([j.sets for j in jobs])
+                if all(j.idx is not None for j in jobs):
+                    codes = self.engine.verify_jobs_indexed([j.sets for j in jobs], [j.idx for j in jobs])
+                else:
+                    codes = self.engine.verify_jobs([j.sets for j in jobs])
                 err = None
             except Exception as e:  # device failure: every job of the package rejects (index.ts:368-375)
                 codes, err = None, e

@@ -48,9 +48,10 @@ class SetSpec:
 @dataclass
 class Workload:
     name: str
-    packed: PackedJobs
+    packed: PackedJobs      # carries both 96-byte keys and pk_indices into the key pool
     n_invalid_jobs: int
     expected: np.ndarray    # per job 1 / 0
+    pool96: Optional[np.ndarray] = None  # the key pool (row k = key of index k)
 
 
 class KeyPool:
@@ -92,8 +93,9 @@ def build(engine: Engine, jobs: Sequence[Sequence[SetSpec]], name: str, keys: Op
     pubkeys = np.ascontiguousarray(keys.pk96[vidx].reshape(-1))
     expected = np.array([0 if any(s.invalid for s in j) else 1 for j in jobs], dtype=np.int32)
     packed = PackedJobs(job_off=job_off, pk_off=pk_off, pubkeys=pubkeys, msgs=msgs.reshape(-1).copy(),
-                        sigs=sigs.reshape(-1).copy(), sig_sizes=None)
-    return Workload(name=name, packed=packed, n_invalid_jobs=int((expected == 0).sum()), expected=expected)
+                        sigs=sigs.reshape(-1).copy(), sig_sizes=None, pk_indices=vidx.astype(np.uint32))
+    return Workload(name=name, packed=packed, n_invalid_jobs=int((expected == 0).sum()), expected=expected,
+                    pool96=keys.pk96)
 
 
 def _block(rng, base_v: int, sync_k: int = 358, att_k: int = 256, n_att: int = 128) -> List[SetSpec]:
@@ -146,3 +148,14 @@ SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c4": c4_specs, "c5": c
 def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:
     rng = np.random.default_rng(seed)
     return build(engine, SPECS[name](rng, **kw), name, keys=keys, seed=seed)
+
+
+def indexed_for(engine: Engine, wl: Workload) -> PackedJobs:
+    """Register the workload's key pool in `engine`'s resident table and return the batch with
+    4-byte table indices instead of 96-byte keys (the index2pubkey path)."""
+    base, st = engine.pubkey_table_append([r.tobytes() for r in wl.pool96])
+    if any(st):
+        raise RuntimeError("pubkey table append failed")
+    p = wl.packed
+    return PackedJobs(job_off=p.job_off, pk_off=p.pk_off, pubkeys=None, msgs=p.msgs, sigs=p.sigs,
+                      sig_sizes=p.sig_sizes, pk_indices=(p.pk_indices + np.uint32(base)).astype(np.uint32))

@@ -211,3 +211,67 @@ def test_fp_mul_asm_matches_reference_body():
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert json.loads(out.stdout.strip().splitlines()[-1])["mismatches"] == 0
+
+
+def test_pubkey_table_indexed_batches_match_byte_batches(engine):
+    """GPU-resident pubkey table: index-based sets give the same per-job
+    results as byte-carrying sets; bad indices and bad keys reject their own job only."""
+    from lodestar_amd.engine import PackedJobs
+    k = load_json("reference_kats.json")
+    pk48 = [bytes.fromhex(p) for p in k["K1_interop_pubkeys"]["pubkeys"][:8]]
+    first, st = engine.pubkey_table_append(pk48, validate=True)
+    assert st == [0] * 8
+    # a key that fails decoding (x >= p) and one infinity key
+    bad_first, st2 = engine.pubkey_table_append([bytes([0x9f]) + b"\xff" * 47, bytes([0xc0]) + bytes(47)])
+    assert st2 == [1, 0]
+    jobs = make_batch(engine, 40, agg_k=5, seed=21, invalid={7, 30})
+    packed = pack_jobs(jobs)
+    ref = engine.verify_jobs(jobs)
+    # the same sets expressed as table indices (make_batch draws from a 64-key interop pool)
+    _, pk96 = engine.sk_to_pk([interop_sk(i) for i in range(64)])
+    base, st3 = engine.pubkey_table_append([pk96[i].tobytes() for i in range(64)])
+    assert st3 == [0] * 64
+    lookup = {pk96[i].tobytes(): base + i for i in range(64)}
+    idx = np.array([lookup[packed.pubkeys[96 * j: 96 * j + 96].tobytes()] for j in range(len(packed.pubkeys) // 96)],
+                   dtype=np.uint32)
+    ip = PackedJobs(job_off=packed.job_off, pk_off=packed.pk_off, pubkeys=None, msgs=packed.msgs, sigs=packed.sigs,
+                    sig_sizes=None, pk_indices=idx)
+    b = engine.upload(ip)
+    assert list(b.verify()) == ref == [1] * 7 + [0] + [1] * 22 + [0] + [1] * 9
+    b.free()
+    # bad index / bad key / infinity-only aggregate reject their own jobs
+    idx2 = idx.copy()
+    idx2[0] = 10 ** 6                      # set 0: index out of range
+    idx2[5] = bad_first                    # set 1 (keys 5..9): undecodable key
+    idx2[10:15] = bad_first + 1            # set 2: all infinity -> BLST_PK_IS_INFINITY
+    ip2 = PackedJobs(job_off=packed.job_off, pk_off=packed.pk_off, pubkeys=None, msgs=packed.msgs, sigs=packed.sigs,
+                     sig_sizes=None, pk_indices=idx2)
+    b = engine.upload(ip2)
+    codes = list(b.verify())
+    b.free()
+    assert codes[:3] == [-100, -1, -6] and codes[3:] == ref[3:]
+
+
+def test_pool_with_registered_pubkeys():
+    """BlsGpuVerifier with PublicKeys registered in the resident table (index path) gives the same
+    answers as with raw keys, including a rejecting job in the same package."""
+    from lodestar_amd import verifier as V
+    from lodestar_amd.engine import Engine
+    k4 = load_json("reference_kats.json")["K4_multithread_sets"]["sets"]
+
+    async def main():
+        eng = Engine(0)
+        pool = V.BlsGpuVerifier(engine=eng)
+        pks = pool.register_pubkeys([bytes.fromhex(s["pubkey96"]) for s in k4])
+        assert all(p.index is not None for p in pks)
+        sets = [V.SingleSignatureSet(pks[i], bytes.fromhex(s["signing_root"]), bytes.fromhex(s["signature"]))
+                for i, s in enumerate(k4)]
+        good = [pool.verify_signature_sets(sets, V.VerifySignatureOpts(batchable=True)) for _ in range(6)]
+        wrong = V.SingleSignatureSet(pks[0], sets[1].signing_root, sets[0].signature)
+        bad = pool.verify_signature_sets([wrong], V.VerifySignatureOpts(batchable=True))
+        res = await asyncio.gather(*good, bad)
+        await pool.close()
+        eng.close()
+        return res
+
+    assert asyncio.run(main()) == [True] * 6 + [False]
