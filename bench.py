@@ -21,6 +21,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Each engine drives two HIP streams; HIP's default of 4 hardware queues per process would make
+# the 12 streams of 6 batches in flight share queues (false dependencies between independent
+# batches).  16 queues (HIP reads this at runtime init, before any GPU call below) gives every
+# stream its own.  Measured on MI355X: profiles/r1_inflight_sweep.txt.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import numpy as np  # noqa: E402
 
 
@@ -31,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--exchange", action="store_true", help="RCCL all-gather of Fp12 partials per step")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=6,
                     help="batches in flight per GPU: independent engines (own streams + workspaces) driven by "
                          "one host thread each, like the reference pool's concurrent workers")
     ap.add_argument("--no-cpu-baseline", action="store_true")

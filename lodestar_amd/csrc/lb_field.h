@@ -147,6 +147,49 @@ LB_HD fp fp_mul_body(const fp& a, const fp& b) {
   return fp_reduce_once(o, top);
 }
 
+// Montgomery multiplication on 14 x 28-bit unsaturated limbs (same R = 2^384 contract as
+// fp_mul_body).  With 28-bit limbs every partial product is < 2^56 and a column collects at most
+// 28 of them plus a 2^36 carry, so a 64-bit column accumulator never overflows: each of the 392
+// products is ONE carry-free v_mad_u64_u32 (acc = a*b + acc), against 288 MADs + 288 carry adds
+// for 32-bit limbs, and the rows carry nothing but one shift per row.
+// R stays 2^384 although 14 rows divide by 2^392: the second operand is unpacked as b * 2^8
+// (b * 2^8 < 2^392 fits), so the result is a b 2^8 / 2^392 = a b / R.  For a b < R p the output is
+// below 2p (as for fp_mul_body), and one conditional subtraction finishes it.
+LB_HD uint32_t lb_bits28(const uint32_t* w, int off) {  // bits [off, off + 28) of a 12-word value
+  const int q = off >> 5, r = off & 31;
+  const uint32_t lo = q < 12 ? w[q] : 0u;
+  const uint32_t hi = q + 1 < 12 ? w[q + 1] : 0u;
+  return (r ? ((lo >> r) | (hi << (32 - r))) : lo) & 0x0fffffffu;
+}
+LB_HD fp fp_mul28(const fp& a, const fp& b) {
+  const uint32_t P28[14] = {LB_P28_0, LB_P28_1, LB_P28_2, LB_P28_3, LB_P28_4,  LB_P28_5,  LB_P28_6,
+                            LB_P28_7, LB_P28_8, LB_P28_9, LB_P28_10, LB_P28_11, LB_P28_12, LB_P28_13};
+  uint32_t A[14], B[14];
+  LB_UNROLL for (int k = 0; k < 14; k++) A[k] = lb_bits28(a.v, 28 * k);
+  B[0] = (b.v[0] << 8) & 0x0fffffffu;
+  LB_UNROLL for (int k = 1; k < 14; k++) B[k] = lb_bits28(b.v, 28 * k - 8);
+  uint64_t acc[28];
+  LB_UNROLL for (int k = 0; k < 28; k++) acc[k] = 0;
+  LB_UNROLL for (int i = 0; i < 14; i++) {
+    LB_UNROLL for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)A[i] * B[j];
+    const uint32_t m = ((uint32_t)acc[i] * LB_PINV28) & 0x0fffffffu;
+    LB_UNROLL for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;  // column i is now a multiple of 2^28
+  }
+  uint32_t r[14];
+  LB_UNROLL for (int k = 0; k < 13; k++) {
+    r[k] = (uint32_t)acc[14 + k] & 0x0fffffffu;
+    acc[15 + k] += acc[14 + k] >> 28;
+  }
+  r[13] = (uint32_t)acc[27];  // < 2^18: the value is below 2p < 2^382
+  uint32_t o[12];
+  LB_UNROLL for (int w = 0; w < 12; w++) {
+    const int l = (32 * w) / 28, s = 32 * w - 28 * l;  // s <= 24: two limbs cover a word
+    o[w] = (r[l] >> s) | (r[l + 1] << (28 - s));
+  }
+  return fp_reduce_once(o, 0u);
+}
+
 #if defined(__HIPCC__)
 // Out of line on the GPU: one body shared by every call site keeps the pipeline kernels inside
 // the instruction cache and compile time bounded.  Operands and result travel as 16-wide
@@ -166,11 +209,15 @@ __device__ __forceinline__ fp fp_unpack(lb_v16u a) {
 }
 static __device__ __attribute__((noinline)) lb_v16u fp_mul_v(lb_v16u a, lb_v16u b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  // hand-scheduled MAD chains (lb_fpmul_gfx950.h); bit-identical to fp_mul_body
+#if defined(LB_FPMUL_ASM32)
+  // 32-bit limbs, hand-scheduled MAD + carry chains (lb_fpmul_gfx950.h)
   fp x = fp_unpack(a), y = fp_unpack(b);
   uint32_t o[12], top;
   lbm_mont_mul(o, &top, x.v, y.v);
   return fp_pack(fp_reduce_once(o, top));
+#else
+  return fp_pack(fp_mul28(fp_unpack(a), fp_unpack(b)));
+#endif
 #else
   return fp_pack(fp_mul_body(fp_unpack(a), fp_unpack(b)));
 #endif
@@ -185,7 +232,7 @@ __host__ __device__ __forceinline__ fp fp_mul(const fp& a, const fp& b) {
 #else
 static inline fp fp_mul(const fp& a, const fp& b) {
   LB_COUNT_MUL();
-  return fp_mul_body(a, b);
+  return fp_mul28(a, b);
 }
 #endif
 
@@ -307,10 +354,47 @@ LB_NI fp fp_inv_plain_vt(fp a) {
 // Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
 LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
 LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
-LB_HD bool fp_is_square(const fp& a) {
-  // Legendre symbol a^((p-1)/2) in {0, 1, -1}
-  fp l = fp_pow_const(a, LB_EXP_LEGENDRE, 379);
-  return fp_is_zero(a) || fp_eq(l, fp_one());
+// Quadratic character by the binary Jacobi-symbol algorithm (variable time; every input is
+// public: SSWU on hashed messages).  Works on the Montgomery representation directly:
+// (aR / p) = (a / p) (R / p) and R = 2^384 is a square.  ~400 shift/subtract steps instead of
+// the 570-multiplication Legendre exponentiation a^((p-1)/2).
+LB_NI bool fp_is_square(fp a) {
+  if (fp_is_zero(a)) return true;
+  uint32_t u[12], v[12];
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    u[j] = a.v[j];
+    v[j] = Pl[j];
+  }
+  int t = 1;  // (u / v) * t is the answer; v stays odd
+  while (true) {
+    // remove factors of two from u: (2 / v) = -1 iff v = 3, 5 (mod 8)
+    while (u[0] == 0) {
+      LB_UNROLL for (int j = 0; j < 11; j++) u[j] = u[j + 1];
+      u[11] = 0;  // 2^32 is a square: no sign change
+    }
+    int k = lb_ctz32(u[0]);
+    if (k) {
+      lb_shr(u, k);
+      uint32_t v8 = v[0] & 7u;
+      if ((k & 1) && (v8 == 3u || v8 == 5u)) t = -t;
+    }
+    if (lb_is_one_plain(u)) return t == 1;
+    // both odd: make u >= v by swapping (quadratic reciprocity), then u -= v
+    if (!lb_geq(u, v)) {
+      if ((u[0] & 3u) == 3u && (v[0] & 3u) == 3u) t = -t;
+      LB_UNROLL for (int j = 0; j < 12; j++) {
+        uint32_t x = u[j];
+        u[j] = v[j];
+        v[j] = x;
+      }
+      if (lb_is_one_plain(u)) return t == 1;
+    }
+    lb_sub_in(u, v);
+    bool zero = true;
+    LB_UNROLL for (int j = 0; j < 12; j++) zero &= u[j] == 0;
+    if (zero) return false;  // gcd > 1 cannot happen for prime p and a != 0
+  }
 }
 
 // canonical (non-Montgomery) value compared with (p-1)/2: returns a > (p-1)/2

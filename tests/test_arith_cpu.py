@@ -86,6 +86,15 @@ def test_fp_fp2(L):
         assert L.h_fp2_sgn0(b2(A)) == o.f2_sgn0(A)
 
 
+def test_fp_is_square_jacobi(L):
+    # binary Jacobi symbol (lb_field.h fp_is_square) vs Euler's criterion in the oracle
+    rnd = random.Random(7)
+    vals = [rnd.randrange(P) for _ in range(400)] + [x * x % P for x in range(1, 50)] + [P - 1, 2, 3, 5]
+    got = [bool(L.h_fp_is_square(b48(a))) for a in vals]
+    assert got == [o.fp_is_square(a) for a in vals]
+    assert 150 < sum(got[:400]) < 250
+
+
 def test_fp2_sqrt_special(L):
     rnd = random.Random(2)
     for A in [(rnd.randrange(P), 0), (0, rnd.randrange(P)), (4, 0), (P - 4, 0), (0, 0), (1, 0)]:

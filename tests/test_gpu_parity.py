@@ -202,8 +202,9 @@ def test_pool_multithread_e2e_cases(engine):
 
 
 def test_fp_mul_asm_matches_reference_body():
-    """The inline-asm Montgomery product (lb_fpmul_gfx950.h, used by every kernel) agrees with
-    the portable carry-save form fp_mul_body on 16.4M random and edge-case operands."""
+    """The device Montgomery products -- fp_mul28 (14 x 28-bit limbs, what every kernel's fp_mul
+    runs) and the 32-bit inline-asm form (lb_fpmul_gfx950.h) -- agree with the portable
+    carry-save form fp_mul_body on 16.4M random and edge-case operands."""
     import json
     import os
     import subprocess
