@@ -8,7 +8,9 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblodestar_bls.so")
+# LODESTAR_BLS_LIB points at an alternative build of the same library (A/B of compile options).
+LIB_PATH = os.environ.get("LODESTAR_BLS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                               "liblodestar_bls.so")
 
 # status codes (include/lodestar_bls.h)
 LB_OK = 0

@@ -121,6 +121,7 @@ struct lb_engine {
   } while (0)
 
 static inline uint32_t nblk(uint32_t n) { return (n + LB_TPB - 1) / LB_TPB; }
+static inline uint32_t nblk_inv(uint32_t n) { return (n + LB_INV_TPB - 1) / LB_INV_TPB; }
 
 static int fill_scalars(lb_engine* e, uint32_t n, const uint64_t* user) {
   e->h_scalars.resize(n);
@@ -451,7 +452,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_PK_BLIND, s2);
-      hipLaunchKernelGGL(k_pk_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, nc, b->d_set_chunk_off.as<uint32_t>(),
+      hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s2, n, nc, b->d_set_chunk_off.as<uint32_t>(),
                          e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), b->d_pk_off.as<uint32_t>(),
                          e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
     }
@@ -472,7 +473,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_HASH_FIN, s1);
-      hipLaunchKernelGGL(k_hash_finish, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->q.as<uint32_t>(),
+      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, e->q.as<uint32_t>(),
                          e->h_aff.as<uint32_t>());
     }
     // ---- s2: the sum(r_i sig_i) branch, overlapped with the Miller loops

@@ -60,6 +60,56 @@ __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + 
 
 #include "lb_wave.h"
 
+// ---------------------------------------------------------------- block-wide batch inversion
+// Montgomery's trick across the LB_INV_TPB threads of a block: prefix and suffix products by
+// cross-lane scans inside each wave, ONE field inversion per block (wave 0, on a value that is
+// uniform across its lanes, so the variable-time binary EEA runs without divergence), then
+// z_i^-1 = prefix_{i-1} * suffix_{i+1} * (wave total)^-1.  A per-lane inversion instead runs
+// 64 divergent EEAs per wave: about half of k_pk_blind's instructions before this.
+// Every thread of the block must call it; z must be non-zero (callers pass one for idle lanes).
+#define LB_INV_TPB 64
+__device__ __forceinline__ fp fp_shfl_up(const fp& a, unsigned d) {
+  fp r;
+  LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = __shfl_up(a.v[j], d, 64);
+  return r;
+}
+__device__ __forceinline__ fp fp_shfl_down(const fp& a, unsigned d) {
+  fp r;
+  LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = __shfl_down(a.v[j], d, 64);
+  return r;
+}
+__device__ fp fp_inv_block(const fp& z) {
+  constexpr int NW = LB_INV_TPB / 64;
+  __shared__ uint32_t s_tot[NW][12];
+  __shared__ uint32_t s_inv[12];
+  const unsigned lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  fp pre = z, suf = z;  // inclusive prefix / suffix products within the wave
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    fp t = fp_shfl_up(pre, d);
+    if (lane >= d) pre = fp_mul(pre, t);
+  }
+  for (unsigned d = 1; d < 64; d <<= 1) {
+    fp t = fp_shfl_down(suf, d);
+    if (lane + d < 64) suf = fp_mul(suf, t);
+  }
+  if (lane == 63) LB_UNROLL for (int j = 0; j < 12; j++) s_tot[wv][j] = pre.v[j];
+  __syncthreads();
+  if (wv == 0) {
+    fp t = fp_load(s_tot[0]);
+    for (int w = 1; w < NW; w++) t = fp_mul(t, fp_load(s_tot[w]));
+    t = fp_inv(t);
+    if (lane == 0) LB_UNROLL for (int j = 0; j < 12; j++) s_inv[j] = t.v[j];
+  }
+  __syncthreads();
+  fp winv = fp_load(s_inv);  // (product of all wave totals)^-1 -> this wave's total^-1
+  for (int w = 0; w < NW; w++)
+    if (w != (int)wv) winv = fp_mul(winv, fp_load(s_tot[w]));
+  fp pe = fp_shfl_up(pre, 1), se = fp_shfl_down(suf, 1);
+  if (lane == 0) pe = fp_one();
+  if (lane == 63) se = fp_one();
+  return fp_mul(fp_mul(pe, se), winv);
+}
+
 // ---------------------------------------------------------------- signatures
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
@@ -105,15 +155,33 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const 
   soa_st(q, 2 * n, t, p);
 }
 
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
-                                                        uint32_t* __restrict__ h_aff) {
-  uint32_t i = lb_tid();
-  if (i >= n) return;
-  g2j q0 = soa_ld<g2j>(q, 2 * n, i);
-  g2j q1 = soa_ld<g2j>(q, 2 * n, n + i);
-  g2j h = g2_clear_cofactor(jac_add(q0, q1));
+// block of LB_INV_TPB threads (fp_inv_block)
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
+                                                            uint32_t* __restrict__ h_aff) {
+  const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
+  const bool act = i < n;
+  g2j h = jac_infinity<fp2>();
+  if (act) {
+    g2j q0 = soa_ld<g2j>(q, 2 * n, i);
+    g2j q1 = soa_ld<g2j>(q, 2 * n, n + i);
+    h = g2_clear_cofactor(jac_add(q0, q1));
+  }
+  // 1/z = conj(z) / N(z): batch-invert the norm.  H(m) == infinity has negligible probability;
+  // its z = 0 gives x = y = 0 as jac_to_aff would.
+  const fp nz = fp_add(fp_sqr(h.z.c0), fp_sqr(h.z.c1));
+  const bool zero = fp_is_zero(nz);
+  const fp ni = fp_inv_block(zero ? fp_one() : nz);
+  if (!act) return;
   g2a a;
-  jac_to_aff(a, h);  // H(m) == infinity has negligible probability; its z=0 gives x=y=0
+  if (zero) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    const fp2 zi{fp_mul(h.z.c0, ni), fp_neg(fp_mul(h.z.c1, ni))};
+    const fp2 zi2 = fp2_sqr(zi);
+    a.x = fp2_mul(h.x, zi2);
+    a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
+  }
   soa_st(h_aff, n, i, a);
 }
 
@@ -212,32 +280,45 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
 // r * PK for the Miller loop (critical path; the G2 side r * sig is k_sig_blind, off it).
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
-                                                     const uint32_t* __restrict__ chunk_acc,
-                                                     const int32_t* __restrict__ chunk_status,
-                                                     const uint32_t* __restrict__ pk_off,
-                                                     const uint64_t* __restrict__ scalars,
-                                                     uint32_t* __restrict__ rpk_aff,
-                                                     int32_t* __restrict__ pk_status) {
-  uint32_t i = lb_tid();
-  if (i >= n) return;
-  uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
-  int st = (c0 == c1) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
-  g1j acc = jac_infinity<fp>();
-  for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
-    st = chunk_status[c];
-    if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
+// block of LB_INV_TPB threads (fp_inv_block)
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
+                                                         const uint32_t* __restrict__ chunk_acc,
+                                                         const int32_t* __restrict__ chunk_status,
+                                                         const uint32_t* __restrict__ pk_off,
+                                                         const uint64_t* __restrict__ scalars,
+                                                         uint32_t* __restrict__ rpk_aff,
+                                                         int32_t* __restrict__ pk_status) {
+  const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
+  const bool act = i < n;
+  int st = LB_ERR_ARGUMENT;
+  g1j rj = jac_infinity<fp>();
+  if (act) {
+    uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
+    st = (c0 == c1) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+    g1j acc = jac_infinity<fp>();
+    for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
+      st = chunk_status[c];
+      if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
+    }
+    if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
+    if (st == LB_OK) {
+      // a single key's chunk sum is the affine point itself (Z = 1): use mixed additions
+      const bool single = (pk_off[i + 1] - pk_off[i]) == 1;
+      const uint64_t r = scalars[i];
+      rj = single ? jac_mul_u64(g1a{acc.x, acc.y}, r) : jac_mul_u64_jac(acc, r);
+    }
   }
-  if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
-  const bool single = (pk_off[i + 1] - pk_off[i]) == 1;
+  const bool zero = fp_is_zero(rj.z);
+  const fp zi = fp_inv_block(zero ? fp_one() : rj.z);
+  if (!act) return;
   g1a rp;
-  rp.x = fp_zero();
-  rp.y = fp_zero();
-  if (st == LB_OK) {
-    // a single key's chunk sum is the affine point itself (Z = 1): use mixed additions
-    const uint64_t r = scalars[i];
-    g1j rj = single ? jac_mul_u64(g1a{acc.x, acc.y}, r) : jac_mul_u64_jac(acc, r);
-    jac_to_aff(rp, rj);
+  if (st == LB_OK && !zero) {
+    const fp zi2 = fp_sqr(zi);
+    rp.x = fp_mul(rj.x, zi2);
+    rp.y = fp_mul(fp_mul(rj.y, zi2), zi);
+  } else {
+    rp.x = fp_zero();
+    rp.y = fp_zero();
   }
   soa_st(rpk_aff, n, i, rp);
   pk_status[i] = st;
