@@ -90,8 +90,12 @@ uint32_t lb_batch_num_jobs(const lb_batch* b);
 
 /*
  * Verify a resident batch: out_job[n_jobs] receives 1 / 0 / -code per job.
- * scalars: n_sets non-zero 64-bit blinding scalars, or NULL to draw them from the OS
+ * scalars: n_sets non-zero 64-bit blinding words, or NULL to draw them from the OS
  * CSPRNG (getrandom), as blst's verifyMultipleSignatures draws 8 random bytes per set.
+ * A word w = hi:lo stands for the blinding value r = lo + hi * lambda mod q, lambda = -x^2
+ * (the GLV eigenvalue; oracle/bls_oracle.py blinding_scalar).  Like blst's 64-bit integer,
+ * a uniform word is a uniform draw from 2^64 - 1 distinct values, and it halves the blinding
+ * scalar multiplications (lb_curve.h jac_mul_glv).
  * All valid jobs are checked with ONE final exponentiation; a failing batch is bisected
  * over a product tree of jobs down to the invalid ones.
  */

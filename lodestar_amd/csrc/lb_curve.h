@@ -143,6 +143,30 @@ LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
   return acc;
 }
 
+// [r]P for a structured blinding scalar.  The 64-bit word w = hi:lo stands for
+//   r = lo + hi * lambda  (mod q),  lambda = -x^2 mod q,
+// and t1, t2, t3 = P, [lambda]P, P + [lambda]P (affine; free through the endomorphisms, see
+// k_pk_blind / k_sig_blind).  Joint double-and-add over the 32 bit pairs: 32 doublings + 32
+// mixed additions, against 64 + 64 for a plain 64-bit scalar on a wave (the random bits make
+// every wave execute the addition of every step).  The table entry is selected by data, so all
+// lanes follow one path.  Distinct words give distinct r (the lattice {(a, b): a + b lambda = 0
+// mod q} has no non-zero vector with |a|, |b| < 2^32), so a uniform non-zero word is a uniform
+// draw from 2^64 - 1 distinct blinding values, the set size behind blst's 64-bit randomness.
+template <class F>
+LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {
+  jac<F> acc = jac_infinity<F>();
+  for (int i = 31; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    const uint32_t d = (uint32_t)((w >> i) & 1u) | ((uint32_t)((w >> (32 + i)) & 1u) << 1);
+    aff<F> t;
+    t.x = d == 1u ? t1.x : (d == 2u ? t2.x : t3.x);
+    t.y = d == 1u ? t1.y : (d == 2u ? t2.y : t3.y);
+    jac<F> s = jac_add_aff(acc, t);
+    if (d != 0u) acc = s;
+  }
+  return acc;
+}
+
 // [k]P for a 64-bit scalar, P Jacobian (used after aggregation, before the one inversion)
 template <class F>
 LB_NI jac<F> jac_mul_u64_jac(jac<F> p, uint64_t k) {

@@ -301,13 +301,22 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, ui
       if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
     }
     if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
-    if (st == LB_OK) {
-      // a single key's chunk sum is the affine point itself (Z = 1): use mixed additions
-      const bool single = (pk_off[i + 1] - pk_off[i]) == 1;
-      const uint64_t r = scalars[i];
-      rj = single ? jac_mul_u64(g1a{acc.x, acc.y}, r) : jac_mul_u64_jac(acc, r);
-    }
+    rj = acc;
   }
+  // aggregate -> affine (single keys already have Z = 1), one batched inversion per wave
+  const bool ok = act && st == LB_OK;
+  const fp ai = fp_inv_block(ok ? rj.z : fp_one());
+  if (ok) {
+    // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
+    const fp ai2 = fp_sqr(ai);
+    g1a pk;
+    pk.x = fp_mul(rj.x, ai2);
+    pk.y = fp_mul(fp_mul(rj.y, ai2), ai);
+    const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
+    const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
+    rj = jac_mul_glv(pk, t2, t3, scalars[i]);
+  }
+  (void)pk_off;
   const bool zero = fp_is_zero(rj.z);
   const fp zi = fp_inv_block(zero ? fp_one() : rj.z);
   if (!act) return;
@@ -333,7 +342,14 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_blind(uint32_t n, const
   uint32_t i = lb_tid();
   if (i >= n) return;
   g2j rs = jac_infinity<fp2>();
-  if (sig_status[i] == LB_OK && sig_inf[i] == 0u) rs = jac_mul_u64(soa_ld<g2a>(sig_aff, n, i), scalars[i]);
+  if (sig_status[i] == LB_OK && sig_inf[i] == 0u) {
+    // r * sig with r = lo + hi * lambda (k_pk_blind): [lambda]sig = -psi^2(sig) and
+    // sig + [lambda]sig = -psi^4(sig) on G2 (decoded signatures are subgroup-checked)
+    const g2a s = soa_ld<g2a>(sig_aff, n, i);
+    const g2a t2{fp2_mul_fp(s.x, fp_load(LB_PSI2_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI2_CY)))};
+    const g2a t3{fp2_mul_fp(s.x, fp_load(LB_PSI4_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI4_CY)))};
+    rs = jac_mul_glv(s, t2, t3, scalars[i]);
+  }
   soa_st(rsig, n, i, rs);
 }
 

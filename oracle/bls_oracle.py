@@ -799,6 +799,18 @@ def aggregate_pubkeys(pks):
     return acc
 
 
+GLV_LAMBDA = (-BLS_X * BLS_X) % R  # [lambda]P = (beta x, y) on G1, -psi^2 on G2
+
+
+def blinding_scalar(word: int) -> int:
+    """The blinding value a 64-bit scalar word stands for in the HIP engine (lb_curve.h
+    jac_mul_glv): r = lo + hi * lambda mod r_order, lambda = -x^2.  blst draws r as the 64-bit
+    integer itself (maybeBatch.ts:18-25 -> verifyMultipleSignatures); both are uniform draws
+    from 2^64 - 1 distinct non-zero values, so the verdicts agree except with probability
+    2^-64 per invalid batch."""
+    return ((word & 0xFFFFFFFF) + (word >> 32) * GLV_LAMBDA) % R
+
+
 def random_scalar64() -> int:
     while True:
         r = int.from_bytes(os.urandom(8), "little")

@@ -8,6 +8,27 @@ unsigned long long lb_count_mul = 0;
 #include "lb_h2c.h"
 #include "lb_pairing.h"
 
+// fp_inv_block (lb_kernels.h): per element 6 + 6 shuffle-scan multiplications and 2 to combine;
+// the one inversion per wave is a binary EEA (no multiplications) shared by 64 lanes.
+static const unsigned long long INV_BLOCK_MULS = 14;
+// Jacobian -> affine through one fp_inv_block, as k_pk_blind does it (zi^2, x zi^2, y zi^2 zi)
+static void g1_to_aff_block(g1a& out, const g1j& p) {
+  const unsigned long long c = lb_count_mul;
+  jac_to_aff(out, p);
+  lb_count_mul = c + INV_BLOCK_MULS + 4;
+}
+// r * PK / r * sig as k_pk_blind / k_sig_blind compute them (r = lo + hi * lambda, jac_mul_glv)
+static g1j g1_blind(const g1a& pk, uint64_t r) {
+  const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
+  const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
+  return jac_mul_glv(pk, t2, t3, r);
+}
+static g2j g2_blind(const g2a& s, uint64_t r) {
+  const g2a t2{fp2_mul_fp(s.x, fp_load(LB_PSI2_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI2_CY)))};
+  const g2a t3{fp2_mul_fp(s.x, fp_load(LB_PSI4_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI4_CY)))};
+  return jac_mul_glv(s, t2, t3, r);
+}
+
 extern "C" {
 unsigned long long cnt_decode(const uint8_t* sig96) {
   lb_count_mul = 0;
@@ -31,8 +52,11 @@ unsigned long long cnt_hash_finish(const uint8_t* msg) {
   g2j q0 = map_to_curve_g2(fp2{fp_from_be64_words(ub), fp_from_be64_words(ub + 16)});
   g2j q1 = map_to_curve_g2(fp2{fp_from_be64_words(ub + 32), fp_from_be64_words(ub + 48)});
   lb_count_mul = 0;
+  const g2j h = g2_clear_cofactor(jac_add(q0, q1));
+  const unsigned long long c = lb_count_mul;
   g2a a;
-  jac_to_aff(a, g2_clear_cofactor(jac_add(q0, q1)));
+  jac_to_aff(a, h);
+  lb_count_mul = c + 2 + INV_BLOCK_MULS + 2 + 2 + 3 * 3;  // fp2_sqr = 2, fp2_mul = 3 fp muls
   return lb_count_mul;
 }
 // k pubkeys (96 B each), scalar r, signature (for r*sig)
@@ -48,10 +72,11 @@ unsigned long long cnt_pk_blind(const uint8_t* pks, int k, uint64_t r, const uin
     acc = jac_add_aff(acc, p);
     if (i == 0) first = p;
   }
-  g1j rj = k == 1 ? jac_mul_u64(first, r) : jac_mul_u64_jac(acc, r);
-  g1a rp;
-  jac_to_aff(rp, rj);
-  jac_mul_u64(s, r);
+  (void)first;
+  g1a pk, rp;
+  g1_to_aff_block(pk, acc);
+  g1_to_aff_block(rp, g1_blind(pk, r));
+  g2_blind(s, r);
   return lb_count_mul;
 }
 // the two halves of blinding (k_pk_blind: r*PK + affine; k_sig_blind: r*sig)
@@ -59,15 +84,16 @@ unsigned long long cnt_g1_blind(const uint8_t* pk96, uint64_t r) {
   g1a p; bool inf;
   g1_deserialize96(pk96, p, inf);
   lb_count_mul = 0;
-  g1a rp;
-  jac_to_aff(rp, jac_mul_u64(p, r));
+  g1a pk, rp;
+  g1_to_aff_block(pk, jac_from_aff(p));
+  g1_to_aff_block(rp, g1_blind(pk, r));
   return lb_count_mul;
 }
 unsigned long long cnt_g2_blind(const uint8_t* sig96, uint64_t r) {
   g2a s; bool inf;
   g2_decompress96(sig96, s, inf);
   lb_count_mul = 0;
-  jac_mul_u64(s, r);
+  g2_blind(s, r);
   return lb_count_mul;
 }
 unsigned long long cnt_pk_key(const uint8_t* pks, int k) {

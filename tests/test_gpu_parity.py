@@ -113,6 +113,44 @@ def make_batch(engine, n_sets, agg_k=1, seed=1, invalid=()):
     return jobs
 
 
+def test_blinding_words_match_oracle_semantics(engine):
+    """A blinding word w = hi:lo stands for r = lo + hi * lambda (lambda = -x^2; lb_curve.h
+    jac_mul_glv, oracle.blinding_scalar).  On an INVALID batch the root partial depends on r:
+    FE(GPU partial) equals FE of the oracle's prod ML(r PK, H(m)) * ML(-G1, sum r sig) with
+    r = blinding_scalar(w), and differs when the words are read as plain integers."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import bls_oracle as o
+    jobs = make_batch(engine, 3, agg_k=2, seed=33, invalid={1})
+    words = np.array([0x0000000500000003, 0xFFFFFFFF00000001, 0x00000001FFFFFFFF], dtype=np.uint64)
+    b = engine.upload(jobs)
+    try:
+        raw, st = b.partial(words)
+    finally:
+        b.free()
+    assert list(st) == [1, 1, 1]
+    vals = [int.from_bytes(raw[48 * k:48 * (k + 1)], "big") for k in range(12)]
+    f_gpu = tuple(tuple((vals[6 * a + 2 * c], vals[6 * a + 2 * c + 1]) for c in range(3)) for a in range(2))
+
+    def oracle_partial(rs):
+        f, ssum = o.F12_ONE, None
+        for job, r in zip(jobs, rs):
+            (si,) = job
+            pk = None
+            for k in si.pubkeys:
+                pk = o.g1_add(pk, o.g1_deserialize(bytes(k)))
+            sig = o.signature_from_bytes(bytes(si.signature), True)
+            ssum = o.g2_add(ssum, o.g2_mul(sig, r))
+            f = o.f12_mul(f, o.miller_loop(o.g1_mul(pk, r), o.hash_to_g2(bytes(si.signing_root), o.DST_POP)))
+        return o.f12_mul(f, o.miller_loop(o.g1_neg(o.G1), ssum))
+
+    e_gpu = o.final_exponentiation(f_gpu)
+    assert e_gpu != o.F12_ONE
+    assert e_gpu == o.final_exponentiation(oracle_partial([o.blinding_scalar(int(w)) for w in words]))
+    assert e_gpu != o.final_exponentiation(oracle_partial([int(w) for w in words]))
+
+
 def test_bisection_finds_planted_invalid_jobs(engine):
     bad = {3, 77, 200, 201, 511}
     jobs = make_batch(engine, 512, agg_k=1, seed=7, invalid=bad)
