@@ -10,29 +10,27 @@
 #pragma once
 #include "lb_curve.h"
 
-// doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P
+// doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P.
+// 25 Fp multiplications: 3b' = 12(1 + u) is applied with additions, and the output is scaled
+// by 4 (a homogeneous (X:Y:Z) ~ (4X:4Y:4Z)) so the textbook halvings of X3, Y3 disappear.
 LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
-  const fp2 b3 = fp2_load(LB_B2_3);  // 3 b'
   fp2 X = T.x, Y = T.y, Z = T.z;
-  fp2 A = fp2_mul(X, Y);             // XY (halved below)
+  fp2 A = fp2_mul(X, Y);             // XY
   fp2 B = fp2_sqr(Y);
   fp2 C = fp2_sqr(Z);
-  fp2 E = fp2_mul(b3, C);            // 3b' Z^2
+  fp2 E = fp2_mul3(fp2_dbl(fp2_dbl(fp2_mul_xi(C))));  // 3b' Z^2 = 12 (1 + u) Z^2
   fp2 F = fp2_mul3(E);               // 9b' Z^2
-  fp2 G = fp2_add(B, F);             // (B + F), halved below
   fp2 H = fp2_sub(fp2_sqr(fp2_add(Y, Z)), fp2_add(B, C));  // 2YZ
   fp2 XX3 = fp2_mul3(fp2_sqr(X));
   // line: (B - E) + (-3X^2 xP) w^2 + (H yP) w^3
   l0 = fp2_sub(B, E);
   l2 = fp2_neg(fp2_mul_fp(XX3, xP));
   l3 = fp2_mul_fp(H, yP);
-  // X3 = XY/2 (B - F);  Y3 = ((B+F)/2)^2 - 3E^2;  Z3 = B H
-  fp inv2 = fp_load(LB_INV2);
-  fp2 A2 = fp2_mul_fp(A, inv2);
-  fp2 G2 = fp2_mul_fp(G, inv2);
-  T.x = fp2_mul(A2, fp2_sub(B, F));
-  T.y = fp2_sub(fp2_sqr(G2), fp2_mul3(fp2_sqr(E)));
-  T.z = fp2_mul(B, H);
+  // 4 x (X3, Y3, Z3) with X3 = XY/2 (B - F), Y3 = ((B+F)/2)^2 - 3E^2, Z3 = B H:
+  //   X3' = 2 A (B - F),  Y3' = (B + F)^2 - 12 E^2,  Z3' = 4 B H
+  T.x = fp2_dbl(fp2_mul(A, fp2_sub(B, F)));
+  T.y = fp2_sub(fp2_sqr(fp2_add(B, F)), fp2_mul3(fp2_dbl(fp2_dbl(fp2_sqr(E)))));
+  T.z = fp2_dbl(fp2_dbl(fp2_mul(B, H)));
 }
 
 // addition step T <- T + Q (Q affine), line through T and Q at P

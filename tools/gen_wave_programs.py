@@ -269,24 +269,22 @@ def fp12_flat(a):
 # ------------------------------------------------------------ Miller steps (mirror lb_pairing.h)
 def miller_dbl(t, T, xP, yP):
     X, Y, Z = T
-    b3 = (t.pg.const(C_B3), t.pg.const(C_B3 + 1))
-    inv2 = t.pg.const(C_INV2)
     A = t.f2mul(X, Y)
     B = t.f2mat(t.f2sqr(Y))
     C = t.f2mat(t.f2sqr(Z))
-    E = t.f2mat(t.f2mul(b3, C))
+    # 3b' Z^2 = 12 (1 + u) Z^2 (record coefficients stay <= 7: scale in two materialised steps)
+    E = t.f2mat(t.f2mul3(t.f2mat(t.f2dbl(t.f2dbl(t.f2xi(C))))))
     F = t.f2mul3(E)
-    G = t.f2add(B, F)
     H = t.f2mat(t.f2sub(t.f2sqr(t.f2add(Y, Z)), t.f2add(B, C)))
     XX3 = t.f2mul3(t.f2sqr(X))
     l0 = t.f2sub(B, E)
     l2 = t.f2neg(t.f2mulfp(t.f2mat(XX3), xP))
     l3 = t.f2mulfp(H, yP)
-    A2 = t.f2mulfp(t.f2mat(A), inv2)
-    G2 = t.f2mulfp(t.f2mat(G), inv2)
-    X3 = t.f2mul(t.f2mat(A2), t.f2sub(B, F))
-    Y3 = t.f2sub(t.f2sqr(t.f2mat(G2)), t.f2mul3(t.f2sqr(E)))
-    Z3 = t.f2mul(B, H)
+    # output scaled by 4 (no halvings), as lb_pairing.h miller_dbl
+    X3 = t.f2mat(t.f2dbl(t.f2mul(t.f2mat(A), t.f2sub(B, F))))
+    E2x4 = t.f2mat(t.f2dbl(t.f2dbl(t.f2mat(t.f2sqr(E)))))
+    Y3 = t.f2mat(t.f2sub(t.f2sqr(t.f2add(B, F)), t.f2mul3(E2x4)))
+    Z3 = t.f2mat(t.f2dbl(t.f2dbl(t.f2mul(B, H))))
     return (X3, Y3, Z3), (l0, l2, l3)
 
 

@@ -1,5 +1,6 @@
 // Correctness + speed of the device Montgomery products against fp_mul_body (tools/, not product
-// code): fp_mul28 (14 x 28-bit limbs, what fp_mul runs) and the 32-bit inline-asm form.
+// code): fp_mul28 (14 x 28-bit limbs, what fp_mul runs), fp_sqr28 (what fp_sqr runs) and the
+// 32-bit inline-asm form.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include "lb_field.h"
@@ -27,13 +28,16 @@ __global__ void k_check(int n, uint32_t* bad) {
     if (mode == 2) { for (int j = 0; j < 12; j++) b.v[j] = 0; b.v[0] = 1; }
     fp r1 = fp_mul_body(a, b), r2 = mul_asm(a, b), r3 = fp_mul28(a, b);
     for (int j = 0; j < 12; j++) if (r1.v[j] != r2.v[j] || r1.v[j] != r3.v[j]) atomicAdd(bad, 1u);
+    fp q1 = fp_mul_body(a, a), q2 = fp_sqr28(a);
+    for (int j = 0; j < 12; j++) if (q1.v[j] != q2.v[j]) atomicAdd(bad, 1u);
   }
 }
 template <int V>
 __global__ void __launch_bounds__(64) k_speed(uint32_t* out, int iters) {
   fp a, b;
   for (int j = 0; j < 12; j++) { a.v[j] = threadIdx.x * 77 + j; b.v[j] = blockIdx.x + 5 * j; }
-  for (int i = 0; i < iters; i++) a = V == 2 ? fp_mul28(a, b) : V ? mul_asm(a, b) : fp_mul_body(a, b);
+  for (int i = 0; i < iters; i++)
+    a = V == 3 ? fp_sqr28(a) : V == 2 ? fp_mul28(a, b) : V ? mul_asm(a, b) : fp_mul_body(a, b);
   uint32_t x = 0; for (int j = 0; j < 12; j++) x ^= a.v[j];
   out[blockIdx.x * 64 + threadIdx.x] = x;
 }
@@ -49,9 +53,10 @@ int main() {
   uint32_t hb; hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
   printf("{\"mismatches\": %u, \"checked\": %d", hb, 256 * 64 * 1000);
   for (int w : {256, 4096}) {
-    float t0 = run<0>(d, w, 400), t1 = run<1>(d, w, 400), t2 = run<2>(d, w, 400);
-    printf(", \"w%d_body_Gmul_s\": %.2f, \"w%d_asm32_Gmul_s\": %.2f, \"w%d_mul28_Gmul_s\": %.2f", w,
-           w * 64.0 * 400 / t0 / 1e6, w, w * 64.0 * 400 / t1 / 1e6, w, w * 64.0 * 400 / t2 / 1e6);
+    float t0 = run<0>(d, w, 400), t1 = run<1>(d, w, 400), t2 = run<2>(d, w, 400), t3 = run<3>(d, w, 400);
+    printf(", \"w%d_body_Gmul_s\": %.2f, \"w%d_asm32_Gmul_s\": %.2f, \"w%d_mul28_Gmul_s\": %.2f, \"w%d_sqr28_Gsqr_s\": %.2f",
+           w, w * 64.0 * 400 / t0 / 1e6, w, w * 64.0 * 400 / t1 / 1e6, w, w * 64.0 * 400 / t2 / 1e6, w,
+           w * 64.0 * 400 / t3 / 1e6);
   }
   printf("}\n");
   return hb != 0;
