@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--pubkey-bytes", action="store_true", help="ship 96-byte pubkeys instead of table indices")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--no-distinct", action="store_true",
+                    help="skip the secondary measurement with every signing root distinct (c3_distinct)")
     return ap.parse_args()
 
 
@@ -57,12 +59,19 @@ def load_counts():
         return json.load(f)
 
 
+def n_roots(packed):
+    """distinct signing roots in the batch (the grouped path hashes and Miller-loops once per root)"""
+    return int(np.unique(np.asarray(packed.msgs).reshape(-1, 32), axis=0).shape[0]) if packed.n_sets else 0
+
+
 def stage_work(counts, packed):
     """Algorithmic Fp multiplications per pipeline stage for this batch (profiles/roofline_counts.json
-    from tools/count_ops.py: per-item counts of exactly the arithmetic each kernel runs)."""
+    from tools/count_ops.py: per-item counts of exactly the arithmetic each kernel runs).  hash_to_G2
+    and the Miller loop run once per distinct signing root; group_sum is one mixed G1 addition per
+    set plus an affine conversion per root."""
     c = counts["fp_mul_per_item"]
     n = packed.n_sets
-    k = np.diff(packed.pk_off.astype(np.int64))
+    nu = n_roots(packed)
     sets_per_job = np.diff(packed.job_off.astype(np.int64))
     m = 1
     while m < packed.n_jobs:
@@ -70,14 +79,14 @@ def stage_work(counts, packed):
     n_keys = int(packed.pk_off[-1])
     return {
         "decode_sigs": n * c["decode_sigs"],
-        "hash_map": 2 * n * c["hash_map"],
-        "hash_finish": n * c["hash_finish"],
+        "hash_map": 2 * nu * c["hash_map"],
+        "hash_finish": nu * c["hash_finish"],
         "pk_chunks": n_keys * c["pk_key"],
         "pk_blind": n * c["g1_blind"],
         "sig_blind": n * c["g2_blind"],
-        "miller": n * c["miller"],
-        "job_leaves_P": float(((sets_per_job - 1).clip(0) * c["fp12_mul"]).sum()),
-        "tree_up_P": (m - 1) * c["fp12_mul"],
+        "group_sum": n * c["pk_blind_per_extra_key"] + nu * 4,
+        "miller": nu * c["miller"],
+        "tree_up_P": max(nu - 1, 0) * c["fp12_mul"],
         "job_leaves_S": float((sets_per_job * c["g2_add"]).sum()),
         "tree_up_S": (m - 1) * c["g2_add"],
         "ml_S": c["ml_S"],
@@ -104,6 +113,32 @@ def roofline(counts, packed, stage_ms):
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": None,
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}
+
+
+def run_inflight(batches, steps, expected, barrier):
+    """len(batches) batches in flight: independent engines (own streams + workspaces), one host
+    thread each, every engine verifying its own resident copy of the slot `steps` times."""
+    import threading
+    for b in batches[1:]:
+        b.verify()
+    res = [None] * len(batches)
+
+    def run(k):
+        for _ in range(steps):
+            res[k] = batches[k].verify()
+
+    barrier()
+    t1 = time.perf_counter()
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(len(batches))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    barrier()
+    el = time.perf_counter() - t1
+    for r in res:
+        assert np.array_equal(np.asarray(r) == 1, expected == 1), "verification results differ"
+    return el
 
 
 def main():
@@ -180,28 +215,7 @@ def main():
     stage_ms = {k: v / a.steps for k, v in stage_ms.items()}
     el = el_single
     if a.inflight > 1:
-        # (2) `inflight` batches in flight: independent engines (own streams + workspaces), one host
-        # thread each, every engine verifying its own resident copy of the slot K times
-        import threading
-        for b in batches[1:]:
-            b.verify()
-        res = [None] * a.inflight
-
-        def run(k):
-            for _ in range(a.steps):
-                res[k] = batches[k].verify()
-
-        barrier()
-        t1 = time.perf_counter()
-        ths = [threading.Thread(target=run, args=(k,)) for k in range(a.inflight)]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
-        barrier()
-        el = time.perf_counter() - t1
-        for r in res:
-            assert np.array_equal(np.asarray(r) == 1, wl.expected == 1), "verification results differ"
+        el = run_inflight(batches, a.steps, wl.expected, barrier)
     el_t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -214,6 +228,26 @@ def main():
     value = n_sets * world * a.steps * a.inflight / el
 
     roof = roofline(load_counts(), wl.packed, stage_ms)
+    # secondary: the same slot shape with every signing root distinct (no sharing to exploit)
+    value_distinct = None
+    if a.workload == "c3" and not a.no_distinct and not a.exchange:
+        wd = W.make(eng, "c3_distinct", seed=W.SEED + rank)
+        for b in batches:
+            b.free()
+        batches = [e.upload(W.indexed_for(e, wd)) for e in engs]
+        batches[0].verify()
+        eld = run_inflight(batches, a.steps, wd.expected, barrier) if a.inflight > 1 else None
+        if eld is None:
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(a.steps):
+                batches[0].verify()
+            barrier()
+            eld = time.perf_counter() - t1
+        eld_t = torch.tensor([eld], dtype=torch.float64, device=coll_dev)
+        if world > 1:
+            dist.all_reduce(eld_t, op=dist.ReduceOp.MAX)
+        value_distinct = wd.packed.n_sets * world * a.steps * a.inflight / float(eld_t.item())
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -232,8 +266,10 @@ def main():
                        else a.workload, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
                        "pubkeys_per_gpu": int(wl.packed.pk_off[-1]), "parallelism": f"dp{world} (sets sharded)",
                        "exchange": bool(a.exchange), "inflight": a.inflight,
-                       "pubkeys": "96-byte keys per set" if a.pubkey_bytes else "indices into the GPU-resident table"},
+                       "pubkeys": "96-byte keys per set" if a.pubkey_bytes else "indices into the GPU-resident table",
+                       "signing_roots_per_gpu": n_roots(wl.packed)},
             "value_one_batch_in_flight": round(value_single, 1),
+            "value_distinct_roots": None if value_distinct is None else round(value_distinct, 1),
             "roofline": roof, "cpu_baseline": cpu, "gen_s": round(gen_s, 2),
         }), flush=True)
     for e in engs:

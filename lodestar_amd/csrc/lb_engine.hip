@@ -44,29 +44,34 @@ struct dbuf {
 };
 
 // Pipeline stages; (s1) / (s2) = the HIP stream a stage runs on.  s2 carries signature decode,
-// pubkey aggregation + blinding and the whole sum(r_i sig_i) branch; s1 carries hash_to_G2,
-// the per-set Miller loops and the product tree.  They join before the root check.
+// pubkey aggregation + blinding and the whole sum(r_i sig_i) branch; s1 groups the sets by
+// signing root, hashes each distinct root, sums r_i PK_i per root and runs one Miller loop per
+// root into the message product tree.  They join before the root check.  Only a failing root
+// runs the per-set fallback (per-set Miller loops + the job tree) and the bisection.
 enum {
   ST_DECODE = 0,  // s2
+  ST_DEDUP,       // s1
   ST_HASH_MAP,    // s1
   ST_HASH_FIN,    // s1
   ST_PK_CHUNKS,   // s2
   ST_PK_BLIND,    // s2
   ST_SIG_BLIND,   // s2
+  ST_GSUM,        // s1
   ST_MILLER,      // s1
-  ST_LEAVES_P,    // s1
   ST_TREE_P,      // s1
   ST_LEAVES_S,    // s2
   ST_TREE_S,      // s2
   ST_ML_S,        // s2
   ST_ROOT,        // s1 (after joining s2)
+  ST_FALLBACK,    // s1
   ST_BISECT,      // s1
   ST_TOTAL,
   kStages
 };
-const char* const kStageNames[kStages] = {"decode_sigs", "hash_map",     "hash_finish", "pk_chunks",   "pk_blind",
-                                          "sig_blind",   "miller",       "job_leaves_P", "tree_up_P",  "job_leaves_S",
-                                          "tree_up_S",   "ml_S",         "root_check",  "bisect",      "total"};
+const char* const kStageNames[kStages] = {"decode_sigs", "dedup",     "hash_map",  "hash_finish", "pk_chunks",
+                                          "pk_blind",    "sig_blind", "group_sum", "miller",      "tree_up_P",
+                                          "job_leaves_S", "tree_up_S", "ml_S",      "root_check",  "fallback",
+                                          "bisect",      "total"};
 
 }  // namespace
 
@@ -99,6 +104,10 @@ struct lb_engine {
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
       nodes, verdict, parts, ok, chunk_acc, chunk_status, fS;
+  // message grouping (k_msg_*, k_gsum_*)
+  dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
+      set_live, gacc, gp_aff, gp_inf;
+  uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -184,6 +193,8 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   LB_HIP(hipSetDevice(device));
   lb_engine* e = new lb_engine();
   e->device = device;
+  while (getrandom(&e->msg_key, 8, 0) != 8) {
+  }
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete e;
@@ -207,7 +218,10 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamSynchronize(e->stream);
   dbuf* bufs[] = {&e->scalars, &e->sig_aff, &e->sig_inf, &e->sig_status, &e->q, &e->h_aff, &e->rpk, &e->rsig,
                   &e->pk_status, &e->ml, &e->treeP, &e->treeS, &e->job_status, &e->nodes, &e->verdict, &e->parts,
-                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->table_flag};
+                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->table_flag, &e->msg_tab,
+                  &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
+                  &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
+                  &e->gp_inf};
   for (dbuf* b : bufs) b->release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
@@ -401,15 +415,21 @@ struct stage_scope {
   }
 };
 
-// Runs the per-set pipeline on two streams and builds both job trees; leaves fS and treeP
-// ready for the root check on s1.  m = tree leaf count (pow2).
-static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& m) {
+// Runs the batch pipeline on two streams: the job S tree (leaf count mj = pow2 >= jobs) with
+// fS = ML(-G1, S_root) on s2, the message product tree (leaf count mu = pow2 >= sets, leaves
+// [0, n_u) live) on s1, joined on s1 ready for the root check.
+static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
   int st = fill_scalars(e, n, scalars);
   if (st != LB_OK) return st;
-  m = 1;
-  while (m < nj) m <<= 1;
+  mj = 1;
+  while (mj < nj) mj <<= 1;
+  mu = 1;
+  while (mu < n) mu <<= 1;
+  const uint32_t mt = mj > mu ? mj : mu;
   const uint32_t ns = n ? n : 1;
+  uint32_t cap = 64;
+  while (cap < 2 * ns) cap <<= 1;
   LB_HIP(e->scalars.ensure((size_t)ns * 8));
   LB_HIP(e->sig_aff.ensure((size_t)ns * sizeof(g2a)));
   LB_HIP(e->sig_inf.ensure((size_t)ns * 4));
@@ -420,10 +440,19 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->rsig.ensure((size_t)ns * sizeof(g2j)));
   LB_HIP(e->pk_status.ensure((size_t)ns * 4));
   LB_HIP(e->ml.ensure((size_t)ns * sizeof(fp12)));
-  LB_HIP(e->treeP.ensure((size_t)2 * m * sizeof(fp12)));
-  LB_HIP(e->treeS.ensure((size_t)2 * m * sizeof(g2j)));
+  LB_HIP(e->treeP.ensure((size_t)2 * mt * sizeof(fp12)));
+  LB_HIP(e->treeS.ensure((size_t)2 * mj * sizeof(g2j)));
   LB_HIP(e->job_status.ensure((size_t)(nj ? nj : 1) * 4));
   LB_HIP(e->fS.ensure(sizeof(fp12)));
+  LB_HIP(e->msg_tab.ensure((size_t)cap * 4));
+  dbuf* per_set[] = {&e->rep_of, &e->uid_of, &e->uniq_set, &e->set_uid, &e->gcnt, &e->gpos, &e->chunk_beg,
+                     &e->chunk_end, &e->members, &e->set_live, &e->gp_inf};
+  for (dbuf* d : per_set) LB_HIP(d->ensure((size_t)ns * 4));
+  LB_HIP(e->goff.ensure((size_t)(ns + 1) * 4));
+  LB_HIP(e->gch.ensure((size_t)(ns + 1) * 4));
+  LB_HIP(e->n_u.ensure(4));
+  LB_HIP(e->gacc.ensure((size_t)ns * sizeof(g1j)));
+  LB_HIP(e->gp_aff.ensure((size_t)ns * sizeof(g1a)));
   const uint32_t nc = b->n_chunks;
   LB_HIP(e->chunk_acc.ensure((size_t)(nc ? nc : 1) * sizeof(g1j)));
   LB_HIP(e->chunk_status.ensure((size_t)(nc ? nc : 1) * 4));
@@ -437,6 +466,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   // fork: s2 starts after s1's scalar upload
   LB_HIP(hipEventRecord(e->ev_fork, s1));
   LB_HIP(hipStreamWaitEvent(s2, e->ev_fork, 0));
+  const uint32_t* nu = e->n_u.as<uint32_t>();
   if (n) {
     // ---- s2: signatures, pubkeys, r*PK
     {
@@ -456,8 +486,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), b->d_pk_off.as<uint32_t>(),
                          e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
     }
-    LB_HIP(hipEventRecord(e->ev_g1, s2));
-    // signatures: decoded while s1 hashes and runs the Miller loops
+    // signatures: decoded while s1 groups and hashes the messages
     {
       stage_scope sc(e, ST_DECODE, s2);
       hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
@@ -465,15 +494,32 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
     }
     LB_HIP(hipEventRecord(e->ev_dec, s2));
-    // ---- s1: hash_to_G2
+    // ---- s1: group the sets by signing root
+    {
+      stage_scope sc(e, ST_DEDUP, s1);
+      LB_HIP(hipMemsetAsync(e->msg_tab.p, 0xff, (size_t)cap * 4, s1));
+      LB_HIP(hipMemsetAsync(e->n_u.p, 0, 4, s1));
+      LB_HIP(hipMemsetAsync(e->gcnt.p, 0, (size_t)n * 4, s1));
+      hipLaunchKernelGGL(k_msg_insert, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(), e->msg_key,
+                         cap, e->msg_tab.as<uint32_t>(), e->rep_of.as<uint32_t>(), e->uid_of.as<uint32_t>(),
+                         e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
+      hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
+                         e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
+                         e->gpos.as<uint32_t>());
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
+                         e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>());
+      hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
+                         e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
+    }
+    // ---- s1: hash_to_G2 once per distinct root
     {
       stage_scope sc(e, ST_HASH_MAP, s1);
-      hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(),
-                         e->q.as<uint32_t>());
+      hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * n)), dim3(LB_TPB), 0, s1, n, nu, e->uniq_set.as<uint32_t>(),
+                         b->d_msgs.as<uint8_t>(), e->q.as<uint32_t>());
     }
     {
       stage_scope sc(e, ST_HASH_FIN, s1);
-      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, e->q.as<uint32_t>(),
+      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
                          e->h_aff.as<uint32_t>());
     }
     // ---- s2: the sum(r_i sig_i) branch, overlapped with the Miller loops
@@ -483,48 +529,74 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(),
                          e->rsig.as<uint32_t>());
     }
-    // ---- s1: Miller loops (need r*PK and the statuses from s2)
-    LB_HIP(hipStreamWaitEvent(s1, e->ev_g1, 0));
+    // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
+    LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
+    {
+      stage_scope sc(e, ST_GSUM, s1);
+      hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s1, nj, b->d_job_off.as<uint32_t>(),
+                         e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
+                         e->set_live.as<uint32_t>());
+      hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(),
+                         e->set_live.as<uint32_t>(), e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
+      hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                         e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
+    }
     {
       stage_scope sc(e, ST_MILLER, s1);
-      hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rpk.as<uint32_t>(),
-                         e->h_aff.as<uint32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>());
+      hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                         e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+    }
+    {
+      stage_scope sc(e, ST_TREE_P, s1);
+      for (uint32_t lo = mu / 2; lo >= 1; lo /= 2)
+        hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
     }
   } else {
-    LB_HIP(hipEventRecord(e->ev_g1, s2));
+    // no sets: every job is empty; the message tree is the single identity leaf
     LB_HIP(hipEventRecord(e->ev_dec, s2));
+    hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s1, nj, b->d_job_off.as<uint32_t>(),
+                       e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
+                       e->set_live.as<uint32_t>());
+    hipLaunchKernelGGL(k_set_one, dim3(1), dim3(64), 0, s1, e->treeP.as<uint32_t>(), 2 * mu, mu);
   }
   // ---- s2: S tree and ML(-G1, S_root)
   {
     stage_scope sc(e, ST_LEAVES_S, s2);
-    hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(m)), dim3(LB_TPB), 0, s2, nj, n, m, b->d_job_off.as<uint32_t>(),
+    hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(mj)), dim3(LB_TPB), 0, s2, nj, n, mj, b->d_job_off.as<uint32_t>(),
                        e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->rsig.as<uint32_t>(),
                        e->treeS.as<uint32_t>());
   }
   {
     stage_scope sc(e, ST_TREE_S, s2);
-    for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
-      hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s2, m, lo, e->treeS.as<uint32_t>());
+    for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
+      hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s2, mj, lo, e->treeS.as<uint32_t>());
   }
   {
     stage_scope sc(e, ST_ML_S, s2);
-    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, m, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
+    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
   }
   LB_HIP(hipEventRecord(e->ev_s, s2));
-  // ---- s1: P tree (job statuses need the signature decode from s2: recorded as ev_g1 below)
-  LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
-  {
-    stage_scope sc(e, ST_LEAVES_P, s1);
-    hipLaunchKernelGGL(k_job_leaves_P, dim3(nblk(m)), dim3(LB_TPB), 0, s1, nj, n, m, b->d_job_off.as<uint32_t>(),
-                       e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>(),
-                       e->treeP.as<uint32_t>(), e->job_status.as<int32_t>());
-  }
-  {
-    stage_scope sc(e, ST_TREE_P, s1);
-    for (uint32_t lo = m / 2; lo >= 1; lo /= 2)
-      hipLaunchKernelGGL(k_tree_up_P, dim3(lo), dim3(64), 0, s1, m, lo, e->treeP.as<uint32_t>());
-  }
   LB_HIP(hipStreamWaitEvent(s1, e->ev_s, 0));  // join
+  LB_HIP(hipGetLastError());
+  return LB_OK;
+}
+
+// Per-set fallback after a failing root: per-set Miller loops and the job product tree
+// (leaves = jobs, rejecting jobs are identity), the structure the bisection walks.
+static int32_t run_fallback(lb_engine* e, lb_batch* b, uint32_t mj) {
+  const uint32_t n = b->n_sets, nj = b->n_jobs;
+  hipStream_t s1 = e->stream;
+  stage_scope sc(e, ST_FALLBACK, s1);
+  if (n)
+    hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rpk.as<uint32_t>(),
+                       e->h_aff.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->pk_status.as<int32_t>(),
+                       e->ml.as<uint32_t>());
+  hipLaunchKernelGGL(k_job_leaves_P, dim3(nblk(mj)), dim3(LB_TPB), 0, s1, nj, n, mj, b->d_job_off.as<uint32_t>(),
+                     e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>(),
+                     e->treeP.as<uint32_t>(), e->job_status.as<int32_t>());
+  for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
+    hipLaunchKernelGGL(k_tree_up_P, dim3(lo), dim3(64), 0, s1, mj, lo, e->treeP.as<uint32_t>());
   LB_HIP(hipGetLastError());
   return LB_OK;
 }
@@ -561,14 +633,14 @@ extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* sc
   LB_HIP(hipSetDevice(e->device));
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
-  uint32_t m = 1;
-  int32_t st = run_pipeline(e, b, scalars, m);
+  uint32_t m = 1, mu = 1;
+  int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   // root verdict on s1 (after the join)
   LB_HIP(e->verdict.ensure(4));
   {
     stage_scope sc(e, ST_ROOT, e->stream);
-    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->verdict.as<int32_t>());
   }
   LB_HIP(hipGetLastError());
@@ -589,6 +661,9 @@ extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* sc
     if (m == 1) {
       out_job[0] = 0;
     } else {
+      // the job tree's root is the same product as the failed message tree's: start below it
+      st = run_fallback(e, b, m);
+      if (st != LB_OK) return st;
       cand.push_back(2);
       cand.push_back(3);
     }
@@ -644,17 +719,17 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   if (!e || !b || !out576 || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
   std::lock_guard<std::mutex> lk(e->mu);
   LB_HIP(hipSetDevice(e->device));
-  uint32_t m = 1;
+  uint32_t m = 1, mu = 1;
   if (b->n_jobs == 0) {
     fp12_to_be576(out576, fp12_one());
     return LB_OK;
   }
-  int32_t st = run_pipeline(e, b, scalars, m);
+  int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
   {
     stage_scope sc(e, ST_ROOT, e->stream);
-    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, m, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->parts.as<uint8_t>());
   }
   LB_HIP(hipGetLastError());

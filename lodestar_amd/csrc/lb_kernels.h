@@ -138,28 +138,34 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, con
 }
 
 // ---------------------------------------------------------------- hash_to_G2
-// thread t: set t % n, field element u_{t / n}; output Jacobian points q[2n]
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const uint8_t* __restrict__ msgs,
-                                                     uint32_t* __restrict__ q) {
+// Hashing runs once per DISTINCT signing root (k_msg_insert below): thread t handles unique
+// message t % n, field element u_{t / n}, for t % n < *n_u; output Jacobian points q (stride 2n).
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                     const uint32_t* __restrict__ uniq_set,
+                                                     const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
   uint32_t t = lb_tid();
   if (t >= 2 * n) return;
-  uint32_t i = t < n ? t : t - n;
+  uint32_t u = t < n ? t : t - n;
+  if (u >= *n_u) return;
   uint32_t which = t < n ? 0u : 1u;
   uint8_t m[32];
-  ld_bytes<32>(m, msgs + (size_t)32 * i);
+  ld_bytes<32>(m, msgs + (size_t)32 * uniq_set[u]);
   uint32_t ub[64];
   expand_message_xmd_256(ub, m);
   const uint32_t* w = ub + 32 * which;
-  fp2 u{fp_from_be64_words(w), fp_from_be64_words(w + 16)};
-  g2j p = map_to_curve_g2(u);
+  fp2 u2{fp_from_be64_words(w), fp_from_be64_words(w + 16)};
+  g2j p = map_to_curve_g2(u2);
   soa_st(q, 2 * n, t, p);
 }
 
 // block of LB_INV_TPB threads (fp_inv_block)
-__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ q,
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                            const uint32_t* __restrict__ q,
                                                             uint32_t* __restrict__ h_aff) {
   const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
-  const bool act = i < n;
+  const uint32_t nu = *n_u;
+  if (blockIdx.x * LB_INV_TPB >= nu) return;  // whole block idle (uniform: fp_inv_block is safe)
+  const bool act = i < nu;
   g2j h = jac_infinity<fp2>();
   if (act) {
     g2j q0 = soa_ld<g2j>(q, 2 * n, i);
@@ -354,10 +360,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_blind(uint32_t n, const
 }
 
 // ---------------------------------------------------------------- Miller loops
-// Needs only r*PK and H(m): signature decoding runs concurrently on the other stream, and a
-// set whose signature turns out malformed is dropped at the job leaves.
+// Per-set loops ML(r_i PK_i, H(m_i)): only the fallback after a failing grouped root needs them
+// (per-job bisection).  H(m_i) is the hash of the set's unique message (set_uid).
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const uint32_t* __restrict__ rpk_aff,
                                                    const uint32_t* __restrict__ h_aff,
+                                                   const uint32_t* __restrict__ set_uid,
                                                    const int32_t* __restrict__ pk_status,
                                                    uint32_t* __restrict__ ml) {
   uint32_t i = lb_tid();
@@ -365,10 +372,147 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const ui
   fp12 f = fp12_one();
   if (pk_status[i] == LB_OK) {
     g1a p = soa_ld<g1a>(rpk_aff, n, i);
-    g2a h = soa_ld<g2a>(h_aff, n, i);
-    f = miller_loop_inl(p, h);
+    if (!(fp_is_zero(p.x) && fp_is_zero(p.y))) {  // (0, 0): r*PK at infinity, ML = 1
+      g2a h = soa_ld<g2a>(h_aff, n, set_uid[i]);
+      f = miller_loop_inl(p, h);
+    }
   }
   soa_st(ml, n, i, f);
+}
+
+// Grouped loops: ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u
+// (bilinearity: prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into
+// leaf m + u of the message product tree (stride 2m).  Lanes u >= *n_u are idle.
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller_grouped(uint32_t n, uint32_t m,
+                                                           const uint32_t* __restrict__ n_u,
+                                                           const uint32_t* __restrict__ gp_aff,
+                                                           const uint32_t* __restrict__ gp_inf,
+                                                           const uint32_t* __restrict__ h_aff,
+                                                           uint32_t* __restrict__ treeP) {
+  uint32_t u = lb_tid();
+  if (u >= *n_u) return;
+  fp12 f = fp12_one();
+  if (!gp_inf[u]) {
+    g1a p = soa_ld<g1a>(gp_aff, n, u);
+    g2a h = soa_ld<g2a>(h_aff, n, u);
+    f = miller_loop_inl(p, h);
+  }
+  soa_st(treeP, 2 * m, m + u, f);
+}
+
+// ---------------------------------------------------------------- message grouping
+// Sets that sign the same 32-byte root share one hash_to_G2 and one Miller loop (on mainnet a
+// committee's unaggregated attestations all sign one AttestationData root, every aggregator of a
+// slot signs the same selection-proof root, and all 512 sync-committee members sign one block
+// root).  The batch equation is unchanged: prod_i e(r_i PK_i, H(m_i)) regrouped by message.
+//
+// k_msg_insert: open addressing over a table of set indices (capacity cap = pow2 >= 2n, every
+// slot 0xffffffff), probed from a keyed hash of the root (key from the engine's CSPRNG, so crafted
+// roots cannot be aimed at one probe chain); equality is decided on all 32 bytes.  A slot, once
+// claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
+#define LB_GROUP_CHUNK 32  // members summed per lane in k_gsum_chunks
+__device__ __forceinline__ bool msg_eq(const uint8_t* __restrict__ msgs, uint32_t a, uint32_t b) {
+  const uint4* x = reinterpret_cast<const uint4*>(msgs + (size_t)32 * a);
+  const uint4* y = reinterpret_cast<const uint4*>(msgs + (size_t)32 * b);
+  const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+  return ((x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) | (x1.y ^ y1.y) |
+          (x1.z ^ y1.z) | (x1.w ^ y1.w)) == 0u;
+}
+__device__ __forceinline__ uint32_t msg_hash(const uint8_t* __restrict__ msgs, uint32_t i, uint64_t key) {
+  const uint4* x = reinterpret_cast<const uint4*>(msgs + (size_t)32 * i);
+  const uint4 a = x[0], b = x[1];
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint64_t h = key;
+  LB_UNROLL for (int k = 0; k < 8; k++) {
+    h = (h ^ w[k]) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
+  return (uint32_t)(h >> 32);
+}
+__global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t* __restrict__ msgs, uint64_t key,
+                                                       uint32_t cap, uint32_t* __restrict__ tab,
+                                                       uint32_t* __restrict__ rep_of, uint32_t* __restrict__ uid_of,
+                                                       uint32_t* __restrict__ uniq_set, uint32_t* __restrict__ n_u) {
+  const uint32_t i = lb_tid();
+  if (i >= n) return;
+  uint32_t h = msg_hash(msgs, i, key) & (cap - 1u), rep = i;
+  for (uint32_t probe = 0; probe < cap; probe++) {  // cap > n: a free slot always exists
+    const uint32_t old = atomicCAS(&tab[h], 0xffffffffu, i);
+    if (old == 0xffffffffu) break;
+    if (msg_eq(msgs, old, i)) {
+      rep = old;
+      break;
+    }
+    h = (h + 1u) & (cap - 1u);
+  }
+  rep_of[i] = rep;
+  if (rep == i) {
+    const uint32_t u = atomicAdd(n_u, 1u);
+    uid_of[i] = u;
+    uniq_set[u] = i;
+  }
+}
+
+// set_uid[i] = unique-message id of set i; pos[i] = its rank inside the group (cnt zeroed)
+__global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t* __restrict__ rep_of,
+                                                      const uint32_t* __restrict__ uid_of,
+                                                      uint32_t* __restrict__ set_uid, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ pos) {
+  const uint32_t i = lb_tid();
+  if (i >= n) return;
+  const uint32_t u = uid_of[rep_of[i]];
+  set_uid[i] = u;
+  pos[i] = atomicAdd(&cnt[u], 1u);
+}
+
+// One block: exclusive scans of the group sizes (member offsets goff) and of their chunk
+// counts (gch), and the member range of every chunk.  goff[n_u] / gch[n_u] = totals.
+__global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, const uint32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ goff, uint32_t* __restrict__ gch,
+                                                   uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end) {
+  __shared__ uint32_t s_m[1024], s_c[1024];
+  const uint32_t nu = *n_u, t = threadIdx.x, per = (nu + 1023u) / 1024u;
+  const uint32_t a = min(t * per, nu), b = min(a + per, nu);
+  uint32_t sm = 0, sc = 0;
+  for (uint32_t u = a; u < b; u++) {
+    sm += cnt[u];
+    sc += (cnt[u] + LB_GROUP_CHUNK - 1) / LB_GROUP_CHUNK;
+  }
+  s_m[t] = sm;
+  s_c[t] = sc;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t vm = t >= d ? s_m[t - d] : 0u, vc = t >= d ? s_c[t - d] : 0u;
+    __syncthreads();
+    s_m[t] += vm;
+    s_c[t] += vc;
+    __syncthreads();
+  }
+  uint32_t om = s_m[t] - sm, oc = s_c[t] - sc;
+  for (uint32_t u = a; u < b; u++) {
+    const uint32_t c = cnt[u];
+    goff[u] = om;
+    gch[u] = oc;
+    for (uint32_t k = 0; k < c; k += LB_GROUP_CHUNK) {
+      chunk_beg[oc] = om + k;
+      chunk_end[oc] = om + min(k + LB_GROUP_CHUNK, c);
+      oc++;
+    }
+    om += c;
+  }
+  if (t == 1023) {
+    goff[nu] = s_m[1023];
+    gch[nu] = s_c[1023];
+  }
+}
+
+__global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32_t* __restrict__ set_uid,
+                                                        const uint32_t* __restrict__ pos,
+                                                        const uint32_t* __restrict__ goff,
+                                                        uint32_t* __restrict__ members) {
+  const uint32_t i = lb_tid();
+  if (i >= n) return;
+  members[goff[set_uid[i]] + pos[i]] = i;
 }
 
 // ---------------------------------------------------------------- per-job leaves
@@ -384,6 +528,92 @@ __device__ __forceinline__ int job_status_of(uint32_t a, uint32_t e, const int32
   for (uint32_t i = a; i < e && st == LB_OK; i++)
     if (pk_status[i] != LB_OK) st = pk_status[i];
   return st;
+}
+
+// job_status[j] and, for each of its sets, whether the set takes part in the batch equation
+__global__ void __launch_bounds__(LB_TPB) k_job_status(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
+                                                       const int32_t* __restrict__ sig_status,
+                                                       const int32_t* __restrict__ pk_status,
+                                                       int32_t* __restrict__ job_status,
+                                                       uint32_t* __restrict__ set_live) {
+  const uint32_t j = lb_tid();
+  if (j >= n_jobs) return;
+  const uint32_t a = job_off[j], e = job_off[j + 1];
+  const int st = job_status_of(a, e, sig_status, pk_status);
+  job_status[j] = st;
+  for (uint32_t i = a; i < e; i++) set_live[i] = st == LB_OK ? 1u : 0u;
+}
+
+// chunk c of a group: Jacobian sum of r_i PK_i over its live members -> gacc (stride n)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_gsum_chunks(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                        const uint32_t* __restrict__ gch,
+                                                        const uint32_t* __restrict__ chunk_beg,
+                                                        const uint32_t* __restrict__ chunk_end,
+                                                        const uint32_t* __restrict__ members,
+                                                        const uint32_t* __restrict__ set_live,
+                                                        const uint32_t* __restrict__ rpk_aff,
+                                                        uint32_t* __restrict__ gacc) {
+  const uint32_t c = lb_tid();
+  if (c >= gch[*n_u]) return;
+  g1j acc = jac_infinity<fp>();
+  for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
+    const uint32_t i = members[k];
+    if (!set_live[i]) continue;
+    const g1a p = soa_ld<g1a>(rpk_aff, n, i);
+    if (fp_is_zero(p.x) && fp_is_zero(p.y)) continue;  // r*PK at infinity
+    acc = jac_add_aff(acc, p);
+  }
+  soa_st(gacc, n, c, acc);
+}
+
+// P_u = sum of the group's chunk sums, to affine (one batched inversion per block); gp_inf[u]
+// flags P_u = infinity (no live member, or members cancelling), whose Miller value is 1.
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                           const uint32_t* __restrict__ gch,
+                                                           const uint32_t* __restrict__ gacc,
+                                                           uint32_t* __restrict__ gp_aff,
+                                                           uint32_t* __restrict__ gp_inf) {
+  const uint32_t u = blockIdx.x * LB_INV_TPB + threadIdx.x;
+  const uint32_t nu = *n_u;
+  if (blockIdx.x * LB_INV_TPB >= nu) return;  // whole block idle (uniform)
+  const bool act = u < nu;
+  g1j acc = jac_infinity<fp>();
+  if (act)
+    for (uint32_t c = gch[u]; c < gch[u + 1]; c++) acc = jac_add(acc, soa_ld<g1j>(gacc, n, c));
+  const bool zero = jac_is_inf(acc);
+  const fp zi = fp_inv_block(act && !zero ? acc.z : fp_one());
+  if (!act) return;
+  g1a a;
+  if (zero) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  } else {
+    const fp zi2 = fp_sqr(zi);
+    a.x = fp_mul(acc.x, zi2);
+    a.y = fp_mul(fp_mul(acc.y, zi2), zi);
+  }
+  soa_st(gp_aff, n, u, a);
+  gp_inf[u] = zero ? 1u : 0u;
+}
+
+// element e of an Fp12 SoA array (stride n) <- 1
+__global__ void __launch_bounds__(64) k_set_one(uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
+  if (threadIdx.x == 0) soa_st(base, n, e, fp12_one());
+}
+
+// Message product tree, one level: like k_tree_up_P, but only leaves [0, *n_u) exist.  A node
+// whose leaf range starts at or past *n_u is never read; one whose right half does is a copy.
+__global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const uint32_t* __restrict__ n_u,
+                                                  uint32_t* __restrict__ treeP) {
+  __shared__ fp S[LBW_SLOTS];
+  const uint32_t i = lo + blockIdx.x, span = m / lo, start = blockIdx.x * span, nu = *n_u;
+  if (start >= nu) return;
+  w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
+  if (start + span / 2 < nu) {
+    w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
+    w_mul(S, LBW_A(0), LBW_A(0), LBW_A(1));
+  }
+  w_store_soa12(S, LBW_A(0), treeP, 2 * m, i);
 }
 
 // P_j = prod ML_i over the job's sets (identity for a rejecting job) -> treeP leaf m + j

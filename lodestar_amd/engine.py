@@ -280,8 +280,8 @@ class Engine:
         _check(self.lib.lb_engine_set_profiling(self.h, 1 if on else 0))
 
     def last_profile(self) -> dict:
-        names = (ctypes.c_char_p * 16)()
-        ms = (ctypes.c_float * 16)()
+        names = (ctypes.c_char_p * 32)()
+        ms = (ctypes.c_float * 32)()
         n = ctypes.c_int32(0)
-        _check(self.lib.lb_engine_last_profile(self.h, names, ms, 16, ctypes.byref(n)))
+        _check(self.lib.lb_engine_last_profile(self.h, names, ms, 32, ctypes.byref(n)))
         return {names[i].decode(): float(ms[i]) for i in range(n.value)}

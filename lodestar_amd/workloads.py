@@ -3,7 +3,10 @@
 Keys follow the reference's perf convention: validator v uses interop key v mod 100
 (packages/state-transition/test/perf/util.ts:49-71; interop sk formula
 packages/state-transition/src/util/interop.ts:19-23).  Signing roots are
-sha256(seed || type || slot || index).  Signatures are produced on the GPU with the engine's
+sha256(seed || type || key): sets that sign the same object on mainnet share a key (a committee's
+unaggregated attestations and its aggregates sign one AttestationData; every aggregator of a slot
+signs the same selection-proof slot; the sync committee signs one block root), every other set
+gets its own root.  Signatures are produced on the GPU with the engine's
 synthetic-data kernels (SecretKey.sign); an aggregate signature is (sum sk_i mod r) * H(m).
 
 Shapes (jobs = verifySignatureSets calls after chunkifyMaximizeChunkSize(sets, 128)):
@@ -12,7 +15,10 @@ Shapes (jobs = verifySignatureSets calls after chunkifyMaximizeChunkSize(sets, 1
       (k=358), one non-batchable call of 131 sets (configs[1])
   c3  gossip flood per slot: 16384 attestation calls (1 set, k=1, batchable) + 1024
       aggregate-and-proof calls (2 singles + 1 aggregate k=256)  = 17408 jobs, 19456 sets
-      (configs[2])
+      (configs[2]).  Roots: 64 committees, each voting for the majority head (95 %) or one
+      alternative (5 %) -> <= 128 attestation roots; 1 selection-proof root per slot; 1024
+      distinct AggregateAndProof roots; aggregates carry their committee's majority root.
+      c3_distinct: the same shape with all 19456 roots distinct (the no-sharing bound).
   c4  sync committee: 512 single sync-committee messages + 64 contribution calls (2 singles +
       k=128) + block sync aggregate (k=512) + 4 light-client update aggregates (k=512), with
       one invalid set per 1000 (configs[3])
@@ -43,6 +49,7 @@ class SetSpec:
     validators: List[int]   # pubkey indices (validator ids)
     kind: int               # domain-ish tag for the signing root
     invalid: bool = False   # sign a different message (well-formed, wrong)
+    root: Optional[int] = None  # sets with equal (kind, root) sign the same message; None = own root
 
 
 @dataclass
@@ -74,8 +81,9 @@ def build(engine: Engine, jobs: Sequence[Sequence[SetSpec]], name: str, keys: Op
     msgs = np.zeros((n, 32), dtype=np.uint8)
     sks = []
     for i, s in enumerate(flat):
+        tag = (b"\x01" + s.root.to_bytes(8, "little")) if s.root is not None else (b"\x00" + i.to_bytes(8, "little"))
         msgs[i] = np.frombuffer(hashlib.sha256(seed.to_bytes(8, "little") + s.kind.to_bytes(2, "little")
-                                               + i.to_bytes(8, "little")).digest(), np.uint8)
+                                               + tag).digest(), np.uint8)
         sks.append(sum(keys.sk(v) for v in s.validators) % R or 1)
     sign_msgs = msgs.copy()
     for i, s in enumerate(flat):
@@ -114,20 +122,35 @@ def c2_specs(rng):
     return [_block(rng, 7)]
 
 
-def c3_specs(rng, n_att: int = 16384, n_agg: int = 1024, agg_k: int = 256):
-    jobs = [[SetSpec([int(rng.integers(0, 1 << 20))], 3)] for _ in range(n_att)]
-    for _ in range(n_agg):
+def c3_specs(rng, n_att: int = 16384, n_agg: int = 1024, agg_k: int = 256, committees: int = 64,
+             minority: float = 0.05, shared: bool = True):
+    def att_root(c, alt):
+        return 2 * c + alt if shared else None
+
+    jobs = [[SetSpec([int(rng.integers(0, 1 << 20))], 3,
+                     root=att_root(int(rng.integers(0, committees)), int(rng.random() < minority)))]
+            for _ in range(n_att)]
+    for a in range(n_agg):
         v = int(rng.integers(0, 1 << 20))
-        jobs.append([SetSpec([v], 5), SetSpec([v], 6), SetSpec([int(x) for x in rng.integers(0, 1 << 20, agg_k)], 3)])
+        jobs.append([SetSpec([v], 5, root=0 if shared else None), SetSpec([v], 6),
+                     SetSpec([int(x) for x in rng.integers(0, 1 << 20, agg_k)], 3,
+                             root=att_root(a % committees, 0))])
     return jobs
 
 
+def c3_distinct_specs(rng, **kw):
+    return c3_specs(rng, shared=False, **kw)
+
+
 def c4_specs(rng, invalid_rate: float = 1e-3):
-    jobs = [[SetSpec([int(rng.integers(0, 512))], 7)] for _ in range(512)]
-    for _ in range(64):
+    # sync-committee messages and contributions sign this slot's block root; selection proofs
+    # sign (slot, subcommittee); the block's sync aggregate signs the previous block root
+    jobs = [[SetSpec([int(rng.integers(0, 512))], 7, root=0)] for _ in range(512)]
+    for c in range(64):
         v = int(rng.integers(0, 512))
-        jobs.append([SetSpec([v], 8), SetSpec([v], 9), SetSpec([int(x) for x in rng.integers(0, 512, 128)], 7)])
-    jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 7)])
+        jobs.append([SetSpec([v], 8, root=c % 4), SetSpec([v], 9),
+                     SetSpec([int(x) for x in rng.integers(0, 512, 128)], 7, root=0)])
+    jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 7, root=1)])
     for _ in range(4):
         jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 10)])
     n_sets = sum(len(j) for j in jobs)
@@ -142,7 +165,8 @@ def c5_specs(rng, n_blocks: int = 32):
     return [_block(rng, 11 + b) for b in range(n_blocks)]
 
 
-SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c4": c4_specs, "c5": c5_specs}
+SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c3_distinct": c3_distinct_specs, "c4": c4_specs,
+         "c5": c5_specs}
 
 
 def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:

@@ -314,3 +314,86 @@ def test_pool_with_registered_pubkeys():
         return res
 
     assert asyncio.run(main()) == [True] * 6 + [False]
+
+
+# ---------------------------------------------------------------- sets sharing a signing root
+def make_shared_batch(engine, n_sets, n_msgs, agg_k=1, seed=1, invalid=(), malformed=()):
+    """n_sets single-set jobs whose signing roots are drawn from n_msgs distinct roots (a
+    committee's attestations sign one AttestationData root).  `invalid`: signed over another
+    root (well-formed, wrong); `malformed`: compression flag cleared (BLST_BAD_ENCODING)."""
+    rng = np.random.default_rng(seed)
+    pool = [interop_sk(i) for i in range(64)]
+    _, pk96 = engine.sk_to_pk(pool)
+    roots = rng.integers(0, 256, size=(n_msgs, 32), dtype=np.uint8)
+    which = rng.integers(0, n_msgs, size=n_sets)
+    msgs = roots[which]
+    idx = rng.integers(0, 64, size=(n_sets, agg_k))
+    sks = [sum(pool[j] for j in row) % R for row in idx]
+    sign_msgs = msgs.copy()
+    for i in invalid:
+        sign_msgs[i, 0] ^= 1
+    sigs = engine.sign(sks, sign_msgs)
+    jobs = []
+    for i in range(n_sets):
+        s = bytearray(sigs[i].tobytes())
+        if i in malformed:
+            s[0] &= 0x7F
+        jobs.append([SetInput([pk96[j].tobytes() for j in idx[i]], msgs[i].tobytes(), bytes(s))])
+    return jobs
+
+
+def _verify_profiled(engine, jobs):
+    engine.set_profiling(True)
+    try:
+        codes = engine.verify_jobs(jobs)
+        prof = engine.last_profile()
+    finally:
+        engine.set_profiling(False)
+    return codes, prof
+
+
+def test_shared_roots_grouped_path_accepts(engine):
+    # 700 sets over 5 roots: groups of ~140 span several LB_GROUP_CHUNK chunks; aggregates mixed in
+    jobs = make_shared_batch(engine, 700, 5, agg_k=3, seed=21)
+    codes, prof = _verify_profiled(engine, jobs)
+    assert codes == [1] * 700
+    assert prof["fallback"] == 0.0 and prof["bisect"] >= 0.0
+
+
+def test_shared_roots_invalid_member_found_by_fallback(engine):
+    bad = {0, 13, 399}
+    jobs = make_shared_batch(engine, 400, 3, seed=22, invalid=bad)
+    codes, prof = _verify_profiled(engine, jobs)
+    assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
+    assert all(codes[i] == 0 for i in bad)
+    assert prof["fallback"] > 0.0
+
+
+def test_shared_roots_malformed_job_excluded_without_fallback(engine):
+    from lodestar_amd import _native as N
+    mal = {7, 150}
+    jobs = make_shared_batch(engine, 300, 2, seed=23, malformed=mal)
+    codes, prof = _verify_profiled(engine, jobs)
+    for i, c in enumerate(codes):
+        if i in mal:
+            assert N.error_name(-c) == "BLST_BAD_ENCODING"
+        else:
+            assert c == 1
+    assert prof["fallback"] == 0.0  # rejected jobs leave the per-root sums; the root still passes
+
+
+def test_shared_roots_inside_one_job_and_duplicate_sets(engine):
+    jobs = make_shared_batch(engine, 64, 2, agg_k=2, seed=24)
+    multi = [sum(jobs[i:i + 16], []) for i in range(0, 64, 16)]
+    dup = [jobs[0][0], jobs[0][0]]  # the same set twice in one job (same key, root, signature)
+    assert engine.verify_jobs(multi + [dup] + [jobs[1]]) == [1] * 6
+    bad = make_shared_batch(engine, 64, 2, agg_k=2, seed=24, invalid={37})
+    multi = [sum(bad[i:i + 16], []) for i in range(0, 64, 16)]
+    assert engine.verify_jobs(multi) == [1, 1, 0, 1]
+
+
+def test_all_sets_one_root_and_all_distinct(engine):
+    one = make_shared_batch(engine, 257, 1, seed=25)
+    assert engine.verify_jobs(one) == [1] * 257
+    distinct = make_batch(engine, 257, seed=26, invalid={256})
+    assert engine.verify_jobs(distinct) == [1] * 256 + [0]
