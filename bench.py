@@ -1,16 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark: verified signature sets/s on the mainnet gossip attestation mix (BASELINE.json
-metric; workload c3 = configs[2], one slot's gossip flood: 16384 attestation sets + 1024
-aggregate-and-proof calls x 3 sets, 17408 jobs / 19456 sets per GPU).
+metric; workload c3 = configs[2]: per slot 16384 attestation sets + 1024 aggregate-and-proof calls
+x 3 sets = 17408 jobs / 19456 sets, signing roots shared per committee as on mainnet).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3] [--slots B] [--inflight F]
 
 One process per GPU (torchrun for N>1; RANK/LOCAL_RANK/WORLD_SIZE from the env).  Each rank
-verifies its own slot-sized shard (weak scaling: sets shard across GPUs with no data-path
-collective; the optional --exchange flag adds the 576-byte Fp12 partial all-gather over RCCL
-and one final exponentiation).  A step = lb_batch_verify over the resident
-batch: all kernels + CSPRNG scalars + per-job result readback.  Inputs are in HBM before the
-timed region.  Rank 0 prints one JSON line.
+verifies its own shard (weak scaling: sets shard across GPUs with no data-path collective; the
+optional --exchange flag adds the 576-byte Fp12 partial all-gather over RCCL and one final
+exponentiation).  A batch = B slots of gossip drained into one device batch
+(default 3); F batches are in flight per GPU (default 6, independent engines).  A step =
+lb_batch_verify over one resident batch: all kernels + CSPRNG scalars + per-job result readback.
+Inputs are in HBM before the timed region.  Rank 0 prints one JSON line; value_distinct_roots is
+the same measurement with every signing root distinct (the no-sharing bound).
 """
 import argparse
 import json
@@ -38,6 +40,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c3")
+    ap.add_argument("--slots", type=int, default=3,
+                    help="c3: slots of gossip drained into one device batch (profiles/r1_slots_sweep.txt)")
     ap.add_argument("--exchange", action="store_true", help="RCCL all-gather of Fp12 partials per step")
     ap.add_argument("--inflight", type=int, default=6,
                     help="batches in flight per GPU: independent engines (own streams + workspaces) driven by "
@@ -168,7 +172,8 @@ def main():
     engs = [Engine(local) for _ in range(a.inflight)]
     eng = engs[0]
     t0 = time.time()
-    wl = W.make(eng, a.workload, seed=W.SEED + rank)
+    wkw = {"slots": a.slots} if a.workload.startswith("c3") and a.slots > 1 else {}
+    wl = W.make(eng, a.workload, seed=W.SEED + rank, **wkw)
     gen_s = time.time() - t0
     # pubkeys as indices into each engine's resident table (the epoch cache's index2pubkey path);
     # --pubkey-bytes ships 96-byte keys instead
@@ -231,7 +236,7 @@ def main():
     # secondary: the same slot shape with every signing root distinct (no sharing to exploit)
     value_distinct = None
     if a.workload == "c3" and not a.no_distinct and not a.exchange:
-        wd = W.make(eng, "c3_distinct", seed=W.SEED + rank)
+        wd = W.make(eng, "c3_distinct", seed=W.SEED + rank, **wkw)
         for b in batches:
             b.free()
         batches = [e.upload(W.indexed_for(e, wd)) for e in engs]
@@ -262,13 +267,15 @@ def main():
             "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)", "data": "synthetic",
-            "config": {"workload": f"{a.workload}: gossip attestation flood, one slot per GPU" if a.workload == "c3"
-                       else a.workload, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
+            "config": {"workload": (f"{a.workload}: gossip attestation flood, {a.slots} slot(s) per batch, "
+                                    f"{a.inflight} batches in flight per GPU") if a.workload == "c3" else a.workload,
+                       "slots_per_batch": a.slots, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
                        "pubkeys_per_gpu": int(wl.packed.pk_off[-1]), "parallelism": f"dp{world} (sets sharded)",
                        "exchange": bool(a.exchange), "inflight": a.inflight,
                        "pubkeys": "96-byte keys per set" if a.pubkey_bytes else "indices into the GPU-resident table",
                        "signing_roots_per_gpu": n_roots(wl.packed)},
             "value_one_batch_in_flight": round(value_single, 1),
+            "batch_latency_ms": round(el / a.steps * 1e3, 1),
             "value_distinct_roots": None if value_distinct is None else round(value_distinct, 1),
             "roofline": roof, "cpu_baseline": cpu, "gen_s": round(gen_s, 2),
         }), flush=True)

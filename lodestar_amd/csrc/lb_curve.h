@@ -46,9 +46,13 @@ LB_HD jac<F> jac_neg(const jac<F>& p) {
   return jac<F>{p.x, f_neg(p.y), p.z};
 }
 
+// Group operations come in two forms: jac_*_i is force-inlined (the loop bodies of the scalar
+// multiplications use it, so the point stays in registers; a by-value jac<> argument of an
+// out-of-line call travels through scratch memory), jac_* is the out-of-line wrapper for
+// one-off uses.
 // dbl-2009-l
 template <class F>
-LB_NI jac<F> jac_dbl(jac<F> p) {
+LB_HD jac<F> jac_dbl_i(const jac<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -62,9 +66,14 @@ LB_NI jac<F> jac_dbl(jac<F> p) {
   return r;
 }
 
+template <class F>
+LB_NI jac<F> jac_dbl(jac<F> p) {
+  return jac_dbl_i(p);
+}
+
 // add-2007-bl with the exceptional cases handled
 template <class F>
-LB_NI jac<F> jac_add(jac<F> p, jac<F> q) {
+LB_HD jac<F> jac_add_i(const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.z);
@@ -89,9 +98,14 @@ LB_NI jac<F> jac_add(jac<F> p, jac<F> q) {
   return r;
 }
 
+template <class F>
+LB_NI jac<F> jac_add(jac<F> p, jac<F> q) {
+  return jac_add_i(p, q);
+}
+
 // madd-2007-bl: p Jacobian + q affine (q not infinity)
 template <class F>
-LB_NI jac<F> jac_add_aff(jac<F> p, aff<F> q) {
+LB_HD jac<F> jac_add_aff_i(const jac<F>& p, const aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.z);
   F U2 = f_mul(q.x, Z1Z1);
@@ -111,6 +125,11 @@ LB_NI jac<F> jac_add_aff(jac<F> p, aff<F> q) {
   r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
   r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
   return r;
+}
+
+template <class F>
+LB_NI jac<F> jac_add_aff(jac<F> p, aff<F> q) {
+  return jac_add_aff_i(p, q);
 }
 
 template <class F>
@@ -137,8 +156,8 @@ template <class F>
 LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 63; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k >> i) & 1ull) acc = jac_add_aff(acc, p);
+    acc = jac_dbl_i(acc);
+    if ((k >> i) & 1ull) acc = jac_add_aff_i(acc, p);
   }
   return acc;
 }
@@ -156,12 +175,12 @@ template <class F>
 LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 31; i >= 0; i--) {
-    acc = jac_dbl(acc);
+    acc = jac_dbl_i(acc);
     const uint32_t d = (uint32_t)((w >> i) & 1u) | ((uint32_t)((w >> (32 + i)) & 1u) << 1);
     aff<F> t;
     t.x = d == 1u ? t1.x : (d == 2u ? t2.x : t3.x);
     t.y = d == 1u ? t1.y : (d == 2u ? t2.y : t3.y);
-    jac<F> s = jac_add_aff(acc, t);
+    jac<F> s = jac_add_aff_i(acc, t);
     if (d != 0u) acc = s;
   }
   return acc;
@@ -172,8 +191,8 @@ template <class F>
 LB_NI jac<F> jac_mul_u64_jac(jac<F> p, uint64_t k) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 63; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k >> i) & 1ull) acc = jac_add(acc, p);
+    acc = jac_dbl_i(acc);
+    if ((k >> i) & 1ull) acc = jac_add_i(acc, p);
   }
   return acc;
 }
@@ -184,8 +203,8 @@ template <class F>
 LB_NI jac<F> jac_mul_u256(aff<F> p, const uint32_t* k) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 255; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff(acc, p);
+    acc = jac_dbl_i(acc);
+    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff_i(acc, p);
   }
   return acc;
 }
@@ -195,8 +214,8 @@ template <class F>
 LB_NI jac<F> jac_mul_xabs(jac<F> p) {
   jac<F> acc = p;  // top bit
   for (int i = 62; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((LB_X_ABS >> i) & 1ull) acc = jac_add(acc, p);
+    acc = jac_dbl_i(acc);
+    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_i(acc, p);
   }
   return acc;
 }

@@ -123,7 +123,13 @@ def c2_specs(rng):
 
 
 def c3_specs(rng, n_att: int = 16384, n_agg: int = 1024, agg_k: int = 256, committees: int = 64,
-             minority: float = 0.05, shared: bool = True):
+             minority: float = 0.05, shared: bool = True, slots: int = 1):
+    """`slots` consecutive slots' gossip in one batch (each slot: its own committees and
+    selection-proof root)."""
+    if slots > 1:
+        return [j for s in range(slots) for j in _shift_roots(
+            c3_specs(rng, n_att, n_agg, agg_k, committees, minority, shared), s)]
+
     def att_root(c, alt):
         return 2 * c + alt if shared else None
 
@@ -135,6 +141,14 @@ def c3_specs(rng, n_att: int = 16384, n_agg: int = 1024, agg_k: int = 256, commi
         jobs.append([SetSpec([v], 5, root=0 if shared else None), SetSpec([v], 6),
                      SetSpec([int(x) for x in rng.integers(0, 1 << 20, agg_k)], 3,
                              root=att_root(a % committees, 0))])
+    return jobs
+
+
+def _shift_roots(jobs, slot):
+    for j in jobs:
+        for st in j:
+            if st.root is not None:
+                st.root += slot << 32
     return jobs
 
 
