@@ -72,7 +72,8 @@ def stage_work(counts, packed):
     """Algorithmic Fp multiplications per pipeline stage for this batch (profiles/roofline_counts.json
     from tools/count_ops.py: per-item counts of exactly the arithmetic each kernel runs).  hash_to_G2
     and the Miller loop run once per distinct signing root; group_sum is one mixed G1 addition per
-    set plus an affine conversion per root."""
+    set plus an affine conversion per root; sig_msm is ~8 mixed G2 additions per set (2 points x 4
+    windows of 8 bits, lb_kernels.h k_msm_*; bucket reduction excluded)."""
     c = counts["fp_mul_per_item"]
     n = packed.n_sets
     nu = n_roots(packed)
@@ -87,12 +88,10 @@ def stage_work(counts, packed):
         "hash_finish": nu * c["hash_finish"],
         "pk_chunks": n_keys * c["pk_key"],
         "pk_blind": n * c["g1_blind"],
-        "sig_blind": n * c["g2_blind"],
+        "sig_msm": n * 2 * 4 * c.get("g2_madd", 29),
         "group_sum": n * c["pk_blind_per_extra_key"] + nu * 4,
         "miller": nu * c["miller"],
         "tree_up_P": max(nu - 1, 0) * c["fp12_mul"],
-        "job_leaves_S": float((sets_per_job * c["g2_add"]).sum()),
-        "tree_up_S": (m - 1) * c["g2_add"],
         "ml_S": c["ml_S"],
         "root_check": c["final_exp"] + c["fp12_mul"],
     }
@@ -110,11 +109,24 @@ def roofline(counts, packed, stage_ms):
             t = stage_ms[k] * 1e-3
             per[k] = {"ms": round(stage_ms[k], 3), "fp_mul": int(fm), "tmac_s": round(fm * mac / t / 1e12, 3),
                       "frac": round(fm * mac / t / 1e12 / peak, 4)}
-    dom = max(per, key=lambda k: per[k]["ms"])
+    # dominant kernel = the one carrying the most algorithmic work (the chip's time goes there; the
+    # latency-bound per-root kernels run few waves beside it)
+    dom = max(per, key=lambda k: per[k]["fp_mul"])
     ach = per[dom]["tmac_s"]
     wall = stage_ms.get("total") or sum(stage_ms.values())
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tp):
+        with open(tp) as f:
+            t = json.load(f)
+        k = t.get("kernels", {}).get("k_" + dom)
+        if k and k.get("sets_per_launch") == packed.n_sets:
+            traffic = k["bytes_per_launch"]
     return {"bound": "valu-int", "kernel": "k_" + dom, "achieved": ach, "peak": peak,
-            "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": None,
+            "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": traffic,
+            "traffic_note": "HBM bytes per launch from FETCH_SIZE + WRITE_SIZE (profiles/traffic.json, "
+                            "rocprofv3 --pmc at this config); mostly register-spill scratch: the algorithmic "
+                            "bytes are ~300 B per set (DESIGN.md section 5)",
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}
 

@@ -55,12 +55,10 @@ enum {
   ST_HASH_FIN,    // s1
   ST_PK_CHUNKS,   // s2
   ST_PK_BLIND,    // s2
-  ST_SIG_BLIND,   // s2
+  ST_SIG_MSM,     // s2
   ST_GSUM,        // s1
   ST_MILLER,      // s1
   ST_TREE_P,      // s1
-  ST_LEAVES_S,    // s2
-  ST_TREE_S,      // s2
   ST_ML_S,        // s2
   ST_ROOT,        // s1 (after joining s2)
   ST_FALLBACK,    // s1
@@ -68,10 +66,9 @@ enum {
   ST_TOTAL,
   kStages
 };
-const char* const kStageNames[kStages] = {"decode_sigs", "dedup",     "hash_map",  "hash_finish", "pk_chunks",
-                                          "pk_blind",    "sig_blind", "group_sum", "miller",      "tree_up_P",
-                                          "job_leaves_S", "tree_up_S", "ml_S",      "root_check",  "fallback",
-                                          "bisect",      "total"};
+const char* const kStageNames[kStages] = {"decode_sigs", "dedup",   "hash_map", "hash_finish", "pk_chunks",
+                                          "pk_blind",    "sig_msm", "group_sum", "miller",    "tree_up_P",
+                                          "ml_S",        "root_check", "fallback", "bisect",   "total"};
 
 }  // namespace
 
@@ -107,6 +104,8 @@ struct lb_engine {
   // message grouping (k_msg_*, k_gsum_*)
   dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
       set_live, gacc, gp_aff, gp_inf;
+  // bucket MSM for sum r_i sig_i (k_msm_*)
+  dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum;
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -221,7 +220,8 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->table_flag, &e->msg_tab,
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
-                  &e->gp_inf};
+                  &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum};
   for (dbuf* b : bufs) b->release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
@@ -453,6 +453,17 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->n_u.ensure(4));
   LB_HIP(e->gacc.ensure((size_t)ns * sizeof(g1j)));
   LB_HIP(e->gp_aff.ensure((size_t)ns * sizeof(g1a)));
+  const uint32_t bcap = (2 * LB_MSM_W * ns) / LB_GROUP_CHUNK + LB_MSM_NB;  // bucket chunks, upper bound
+  LB_HIP(e->sig_aos.ensure((size_t)ns * sizeof(g2a)));
+  LB_HIP(e->bcnt.ensure((size_t)LB_MSM_NB * 4));
+  LB_HIP(e->bcursor.ensure((size_t)LB_MSM_NB * 4));
+  LB_HIP(e->boff.ensure((size_t)(LB_MSM_NB + 1) * 4));
+  LB_HIP(e->bch.ensure((size_t)(LB_MSM_NB + 1) * 4));
+  LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
+  LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
+  LB_HIP(e->bmembers.ensure((size_t)2 * LB_MSM_W * ns * 4));
+  LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
+  LB_HIP(e->bsum.ensure((size_t)LB_MSM_NB * sizeof(g2j)));
   const uint32_t nc = b->n_chunks;
   LB_HIP(e->chunk_acc.ensure((size_t)(nc ? nc : 1) * sizeof(g1j)));
   LB_HIP(e->chunk_status.ensure((size_t)(nc ? nc : 1) * 4));
@@ -491,7 +502,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       stage_scope sc(e, ST_DECODE, s2);
       hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
                          b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
-                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+                         e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s2, nj, b->d_job_off.as<uint32_t>(),
+                         e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
+                         e->set_live.as<uint32_t>());
     }
     LB_HIP(hipEventRecord(e->ev_dec, s2));
     // ---- s1: group the sets by signing root
@@ -506,7 +520,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
                          e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
                          e->gpos.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
                          e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
@@ -522,20 +536,31 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
                          e->h_aff.as<uint32_t>());
     }
-    // ---- s2: the sum(r_i sig_i) branch, overlapped with the Miller loops
+    // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
     {
-      stage_scope sc(e, ST_SIG_BLIND, s2);
-      hipLaunchKernelGGL(k_sig_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
-                         e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(),
-                         e->rsig.as<uint32_t>());
+      stage_scope sc(e, ST_SIG_MSM, s2);
+      LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)LB_MSM_NB * 4, s2));
+      LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)LB_MSM_NB * 4, s2));
+      hipLaunchKernelGGL(k_msm_count, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
+                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s2, nullptr, (uint32_t)LB_MSM_NB, e->bcnt.as<uint32_t>(),
+                         e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
+                         e->bchunk_end.as<uint32_t>());
+      hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
+                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
+                         e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
+      hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
+                         e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
+                         e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>());
+      hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(LB_MSM_NB)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
+                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>());
+      hipLaunchKernelGGL(k_msm_reduce, dim3(1), dim3(64), 0, s2, e->bsum.as<uint32_t>(), 2 * mj,
+                         e->treeS.as<uint32_t>());
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
     LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
     {
       stage_scope sc(e, ST_GSUM, s1);
-      hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s1, nj, b->d_job_off.as<uint32_t>(),
-                         e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
-                         e->set_live.as<uint32_t>());
       hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(),
                          e->set_live.as<uint32_t>(), e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
@@ -560,18 +585,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                        e->set_live.as<uint32_t>());
     hipLaunchKernelGGL(k_set_one, dim3(1), dim3(64), 0, s1, e->treeP.as<uint32_t>(), 2 * mu, mu);
   }
-  // ---- s2: S tree and ML(-G1, S_root)
-  {
-    stage_scope sc(e, ST_LEAVES_S, s2);
-    hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(mj)), dim3(LB_TPB), 0, s2, nj, n, mj, b->d_job_off.as<uint32_t>(),
-                       e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->rsig.as<uint32_t>(),
-                       e->treeS.as<uint32_t>());
+  if (!n) {
+    // no sets: S_root = infinity
+    hipLaunchKernelGGL(k_g2_set_inf, dim3(1), dim3(64), 0, s2, e->treeS.as<uint32_t>(), 2 * mj, 1u);
   }
-  {
-    stage_scope sc(e, ST_TREE_S, s2);
-    for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
-      hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s2, mj, lo, e->treeS.as<uint32_t>());
-  }
+  // ---- s2: ML(-G1, S_root)
   {
     stage_scope sc(e, ST_ML_S, s2);
     hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
@@ -597,6 +615,16 @@ static int32_t run_fallback(lb_engine* e, lb_batch* b, uint32_t mj) {
                      e->treeP.as<uint32_t>(), e->job_status.as<int32_t>());
   for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
     hipLaunchKernelGGL(k_tree_up_P, dim3(lo), dim3(64), 0, s1, mj, lo, e->treeP.as<uint32_t>());
+  // per-job signature sums (the MSM only formed the root)
+  if (n)
+    hipLaunchKernelGGL(k_sig_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->scalars.as<uint64_t>(),
+                       e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(),
+                       e->rsig.as<uint32_t>());
+  hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(mj)), dim3(LB_TPB), 0, s1, nj, n, mj, b->d_job_off.as<uint32_t>(),
+                     e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->rsig.as<uint32_t>(),
+                     e->treeS.as<uint32_t>());
+  for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
+    hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s1, mj, lo, e->treeS.as<uint32_t>());
   LB_HIP(hipGetLastError());
   return LB_OK;
 }

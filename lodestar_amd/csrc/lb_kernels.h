@@ -115,6 +115,7 @@ __device__ fp fp_inv_block(const fp& z) {
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                         const uint32_t* __restrict__ sig_sizes,
                                                         uint32_t* __restrict__ sig_aff,
+                                                        uint4* __restrict__ sig_aos,
                                                         uint32_t* __restrict__ sig_inf,
                                                         int32_t* __restrict__ sig_status) {
   uint32_t i = lb_tid();
@@ -133,6 +134,9 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, con
     if (st == LB_OK && !inf && !g2_in_subgroup(jac_from_aff(a))) st = LB_POINT_NOT_IN_GROUP;
   }
   soa_st(sig_aff, n, i, a);
+  // array-of-structures copy (192 B per set) for the MSM's gathers: one point = 12 x 16 B
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+  LB_UNROLL for (int k = 0; k < 12; k++) sig_aos[(size_t)12 * i + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
   sig_inf[i] = inf ? 1u : 0u;
   sig_status[i] = st;
 }
@@ -467,11 +471,13 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t
 
 // One block: exclusive scans of the group sizes (member offsets goff) and of their chunk
 // counts (gch), and the member range of every chunk.  goff[n_u] / gch[n_u] = totals.
-__global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, const uint32_t* __restrict__ cnt,
+// (n_u == nullptr: nu_const groups; the MSM's buckets use it too)
+__global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, uint32_t nu_const,
+                                                   const uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ gch,
                                                    uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end) {
   __shared__ uint32_t s_m[1024], s_c[1024];
-  const uint32_t nu = *n_u, t = threadIdx.x, per = (nu + 1023u) / 1024u;
+  const uint32_t nu = n_u ? *n_u : nu_const, t = threadIdx.x, per = (nu + 1023u) / 1024u;
   const uint32_t a = min(t * per, nu), b = min(a + per, nu);
   uint32_t sm = 0, sc = 0;
   for (uint32_t u = a; u < b; u++) {
@@ -513,6 +519,134 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32
   const uint32_t i = lb_tid();
   if (i >= n) return;
   members[goff[set_uid[i]] + pos[i]] = i;
+}
+
+// ---------------------------------------------------------------- sum r_i sig_i by bucket MSM
+// S = sum over live sets of r_i sig_i with r_i = lo_i + hi_i lambda (k_pk_blind): 2n points
+// (sig_i with scalar lo_i, [lambda]sig_i = -psi^2(sig_i) with hi_i) and 32-bit scalars.
+// Pippenger: LB_MSM_W windows of LB_MSM_C bits; every (point, window) with a non-zero digit d
+// joins bucket (window, d); bucket sums come from chunked Jacobian sums of the members (the
+// message-grouping machinery: count, k_msg_scan, scatter, chunks); one wave then forms
+// sum_d d B_d per window and combines the windows.  About 8 mixed additions per set instead of
+// the 32 doublings + 32 additions of a per-set r*sig; the per-set products (k_sig_blind) are
+// only computed by the fallback, whose bisection needs per-job sums.
+#define LB_MSM_C 8
+#define LB_MSM_W 4
+#define LB_MSM_B (1 << LB_MSM_C)
+#define LB_MSM_NB (LB_MSM_W * LB_MSM_B)  // bucket ids w * 256 + d (d = 0 unused)
+__device__ __forceinline__ bool msm_live(uint32_t i, const uint32_t* set_live, const uint32_t* sig_inf) {
+  return set_live[i] && !sig_inf[i];
+}
+__global__ void __launch_bounds__(LB_TPB) k_msm_count(uint32_t n, const uint64_t* __restrict__ scalars,
+                                                      const uint32_t* __restrict__ set_live,
+                                                      const uint32_t* __restrict__ sig_inf, uint32_t* __restrict__ cnt) {
+  const uint32_t i = lb_tid();
+  if (i >= n || !msm_live(i, set_live, sig_inf)) return;
+  const uint64_t wd = scalars[i];
+  LB_UNROLL for (int h = 0; h < 2; h++) {
+    const uint32_t k = (uint32_t)(wd >> (32 * h));
+    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
+      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+      if (d) atomicAdd(&cnt[w * LB_MSM_B + d], 1u);
+    }
+  }
+}
+__global__ void __launch_bounds__(LB_TPB) k_msm_scatter(uint32_t n, const uint64_t* __restrict__ scalars,
+                                                        const uint32_t* __restrict__ set_live,
+                                                        const uint32_t* __restrict__ sig_inf,
+                                                        const uint32_t* __restrict__ boff, uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ members) {
+  const uint32_t i = lb_tid();
+  if (i >= n || !msm_live(i, set_live, sig_inf)) return;
+  const uint64_t wd = scalars[i];
+  LB_UNROLL for (int h = 0; h < 2; h++) {
+    const uint32_t k = (uint32_t)(wd >> (32 * h));
+    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
+      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+      if (d) {
+        const uint32_t b = w * LB_MSM_B + d;
+        members[boff[b] + atomicAdd(&cursor[b], 1u)] = i | ((uint32_t)h << 31);
+      }
+    }
+  }
+}
+// chunk c of a bucket: Jacobian sum of its member points (AoS affine signatures; bit 31 of a
+// member = the [lambda] image)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_chunks(const uint32_t* __restrict__ bch,
+                                                       const uint32_t* __restrict__ chunk_beg,
+                                                       const uint32_t* __restrict__ chunk_end,
+                                                       const uint32_t* __restrict__ members,
+                                                       const uint4* __restrict__ sig_aos, uint32_t cap,
+                                                       uint32_t* __restrict__ bacc) {
+  const uint32_t c = lb_tid();
+  if (c >= bch[LB_MSM_NB]) return;
+  g2j acc = jac_infinity<fp2>();
+  for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
+    const uint32_t m = members[k], i = m & 0x7fffffffu;
+    g2a p;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&p);
+    LB_UNROLL for (int q = 0; q < 12; q++) {
+      const uint4 v = sig_aos[(size_t)12 * i + q];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+    if (m >> 31) {
+      p.x = fp2_mul_fp(p.x, fp_load(LB_PSI2_CX));
+      p.y = fp2_neg(fp2_mul_fp(p.y, fp_load(LB_PSI2_CY)));
+    }
+    acc = jac_add_aff_i(acc, p);
+  }
+  soa_st(bacc, cap, c, acc);
+}
+// bucket b = sum of its chunk sums (SoA, stride LB_MSM_NB); empty buckets are infinity
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t* __restrict__ bch,
+                                                        const uint32_t* __restrict__ bacc, uint32_t cap,
+                                                        uint32_t* __restrict__ bsum) {
+  const uint32_t b = lb_tid();
+  if (b >= LB_MSM_NB) return;
+  g2j acc = jac_infinity<fp2>();
+  for (uint32_t c = bch[b]; c < bch[b + 1]; c++) acc = jac_add_i(acc, soa_ld<g2j>(bacc, cap, c));
+  soa_st(bsum, LB_MSM_NB, b, acc);
+}
+// One wave: lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
+// Y = sum_j j B_{16s+j} and T = sum_j B_{16s+j}; Y + 16 s T is the segment's share of
+// sum_d d B_d.  Segments then add up in an LDS tree, and the windows combine Horner-style:
+// S = sum_w 2^(8w) W_w  -> treeS node 1 (stride n2m), where k_ml_S reads S_root.
+__global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t n2m,
+                                                   uint32_t* __restrict__ treeS) {
+  static_assert(LB_MSM_W * 16 == 64 && LB_MSM_B == 256, "one lane per 16-digit segment");
+  __shared__ g2j sh[64];
+  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u;
+  g2j run = jac_infinity<fp2>(), y = jac_infinity<fp2>();
+  for (int j = 15; j >= 1; j--) {
+    run = jac_add_i(run, soa_ld<g2j>(bsum, LB_MSM_NB, w * LB_MSM_B + 16 * sg + j));
+    y = jac_add_i(y, run);
+  }
+  if (sg) run = jac_add_i(run, soa_ld<g2j>(bsum, LB_MSM_NB, w * LB_MSM_B + 16 * sg));
+  // y += 16 sg * run   (sg < 16: 4-bit double-and-add, then 4 doublings)
+  g2j t = jac_infinity<fp2>();
+  for (int b = 3; b >= 0; b--) {
+    t = jac_dbl_i(t);
+    if ((sg >> b) & 1u) t = jac_add_i(t, run);
+  }
+  for (int b = 0; b < 4; b++) t = jac_dbl_i(t);
+  y = jac_add_i(y, t);
+  sh[lane] = y;
+  __syncthreads();
+  for (uint32_t d = 8; d >= 1; d >>= 1) {
+    if (sg < d) sh[lane] = jac_add_i(sh[lane], sh[lane + d]);
+    __syncthreads();
+  }
+  if (lane == 0) {
+    g2j S = sh[16 * (LB_MSM_W - 1)];
+    for (int ww = LB_MSM_W - 2; ww >= 0; ww--) {
+      for (int b = 0; b < LB_MSM_C; b++) S = jac_dbl_i(S);
+      S = jac_add_i(S, sh[16 * ww]);
+    }
+    soa_st(treeS, n2m, 1, S);
+  }
 }
 
 // ---------------------------------------------------------------- per-job leaves
@@ -599,6 +733,11 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
 // element e of an Fp12 SoA array (stride n) <- 1
 __global__ void __launch_bounds__(64) k_set_one(uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
   if (threadIdx.x == 0) soa_st(base, n, e, fp12_one());
+}
+
+// element e of a G2 Jacobian SoA array (stride n) <- infinity
+__global__ void __launch_bounds__(64) k_g2_set_inf(uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
+  if (threadIdx.x == 0) soa_st(base, n, e, jac_infinity<fp2>());
 }
 
 // Message product tree, one level: like k_tree_up_P, but only leaves [0, *n_u) exist.  A node

@@ -397,3 +397,12 @@ def test_all_sets_one_root_and_all_distinct(engine):
     assert engine.verify_jobs(one) == [1] * 257
     distinct = make_batch(engine, 257, seed=26, invalid={256})
     assert engine.verify_jobs(distinct) == [1] * 256 + [0]
+
+
+def test_all_valid_distinct_roots_pass_at_the_root(engine):
+    """The bucket MSM for sum r_i sig_i and the per-root sums must reproduce the batch equation
+    exactly: an all-valid batch is accepted by the root check alone (no fallback)."""
+    jobs = make_batch(engine, 300, agg_k=2, seed=27)
+    codes, prof = _verify_profiled(engine, jobs)
+    assert codes == [1] * 300
+    assert prof["fallback"] == 0.0
