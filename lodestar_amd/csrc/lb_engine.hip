@@ -436,7 +436,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->sig_status.ensure((size_t)ns * 4));
   LB_HIP(e->q.ensure((size_t)ns * 2 * sizeof(g2j)));
   LB_HIP(e->h_aff.ensure((size_t)ns * sizeof(g2a)));
-  LB_HIP(e->rpk.ensure((size_t)ns * sizeof(g1a)));
+  LB_HIP(e->rpk.ensure((size_t)ns * sizeof(g1j)));
   LB_HIP(e->rsig.ensure((size_t)ns * sizeof(g2j)));
   LB_HIP(e->pk_status.ensure((size_t)ns * 4));
   LB_HIP(e->ml.ensure((size_t)ns * sizeof(fp12)));

@@ -289,14 +289,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
 }
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
-// r * PK for the Miller loop (critical path; the G2 side r * sig is k_sig_blind, off it).
-// block of LB_INV_TPB threads (fp_inv_block)
+// r * PK (Jacobian) for the per-root sums.  block of LB_INV_TPB threads (fp_inv_block)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
                                                          const uint32_t* __restrict__ chunk_acc,
                                                          const int32_t* __restrict__ chunk_status,
                                                          const uint32_t* __restrict__ pk_off,
                                                          const uint64_t* __restrict__ scalars,
-                                                         uint32_t* __restrict__ rpk_aff,
+                                                         uint32_t* __restrict__ rpk,
                                                          int32_t* __restrict__ pk_status) {
   const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
   const bool act = i < n;
@@ -313,33 +312,32 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, ui
     if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
     rj = acc;
   }
-  // aggregate -> affine (single keys already have Z = 1), one batched inversion per wave
+  // aggregate -> affine for the GLV table.  A single key comes out of its chunk with Z = 1, so a
+  // block of single-key sets (every attestation) skips the batched inversion.
   const bool ok = act && st == LB_OK;
-  const fp ai = fp_inv_block(ok ? rj.z : fp_one());
-  if (ok) {
-    // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
+  const fp one = fp_one();
+  const bool need = ok && !fp_eq(rj.z, one);
+  g1a pk;
+  if (__syncthreads_or(need)) {
+    const fp ai = fp_inv_block(need ? rj.z : one);
     const fp ai2 = fp_sqr(ai);
-    g1a pk;
     pk.x = fp_mul(rj.x, ai2);
     pk.y = fp_mul(fp_mul(rj.y, ai2), ai);
+  } else {
+    pk.x = rj.x;
+    pk.y = rj.y;
+  }
+  if (ok) {
+    // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
     const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
     const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
     rj = jac_mul_glv(pk, t2, t3, scalars[i]);
+  } else {
+    rj = jac_infinity<fp>();
   }
   (void)pk_off;
-  const bool zero = fp_is_zero(rj.z);
-  const fp zi = fp_inv_block(zero ? fp_one() : rj.z);
   if (!act) return;
-  g1a rp;
-  if (st == LB_OK && !zero) {
-    const fp zi2 = fp_sqr(zi);
-    rp.x = fp_mul(rj.x, zi2);
-    rp.y = fp_mul(fp_mul(rj.y, zi2), zi);
-  } else {
-    rp.x = fp_zero();
-    rp.y = fp_zero();
-  }
-  soa_st(rpk_aff, n, i, rp);
+  soa_st(rpk, n, i, rj);
   pk_status[i] = st;
 }
 
@@ -366,7 +364,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_blind(uint32_t n, const
 // ---------------------------------------------------------------- Miller loops
 // Per-set loops ML(r_i PK_i, H(m_i)): only the fallback after a failing grouped root needs them
 // (per-job bisection).  H(m_i) is the hash of the set's unique message (set_uid).
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const uint32_t* __restrict__ rpk_aff,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const uint32_t* __restrict__ rpk,
                                                    const uint32_t* __restrict__ h_aff,
                                                    const uint32_t* __restrict__ set_uid,
                                                    const int32_t* __restrict__ pk_status,
@@ -375,8 +373,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const ui
   if (i >= n) return;
   fp12 f = fp12_one();
   if (pk_status[i] == LB_OK) {
-    g1a p = soa_ld<g1a>(rpk_aff, n, i);
-    if (!(fp_is_zero(p.x) && fp_is_zero(p.y))) {  // (0, 0): r*PK at infinity, ML = 1
+    const g1j pj = soa_ld<g1j>(rpk, n, i);
+    if (!jac_is_inf(pj)) {  // r*PK at infinity: ML = 1
+      g1a p;
+      jac_to_aff(p, pj);
       g2a h = soa_ld<g2a>(h_aff, n, set_uid[i]);
       f = miller_loop_inl(p, h);
     }
@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_gsum_chunks(uint32_t n, con
                                                         const uint32_t* __restrict__ chunk_end,
                                                         const uint32_t* __restrict__ members,
                                                         const uint32_t* __restrict__ set_live,
-                                                        const uint32_t* __restrict__ rpk_aff,
+                                                        const uint32_t* __restrict__ rpk,
                                                         uint32_t* __restrict__ gacc) {
   const uint32_t c = lb_tid();
   if (c >= gch[*n_u]) return;
@@ -693,9 +693,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_gsum_chunks(uint32_t n, con
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t i = members[k];
     if (!set_live[i]) continue;
-    const g1a p = soa_ld<g1a>(rpk_aff, n, i);
-    if (fp_is_zero(p.x) && fp_is_zero(p.y)) continue;  // r*PK at infinity
-    acc = jac_add_aff(acc, p);
+    acc = jac_add_i(acc, soa_ld<g1j>(rpk, n, i));  // r*PK Jacobian (infinity handled)
   }
   soa_st(gacc, n, c, acc);
 }

@@ -406,3 +406,26 @@ def test_all_valid_distinct_roots_pass_at_the_root(engine):
     codes, prof = _verify_profiled(engine, jobs)
     assert codes == [1] * 300
     assert prof["fallback"] == 0.0
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c4", "c5"])
+def test_baseline_config_workloads(engine, name):
+    """BASELINE.json configs as verification batches (lodestar_amd/workloads.py): per-job verdicts
+    equal the planted expectation (c4 carries invalid sets -> fallback + bisection), through both
+    the 96-byte-key and the resident-table paths."""
+    from lodestar_amd import workloads as W
+    wl = W.make(engine, name)
+    b = engine.upload(wl.packed)
+    try:
+        got = np.asarray(b.verify())
+    finally:
+        b.free()
+    assert np.array_equal(got, wl.expected), (name, np.nonzero(got != wl.expected))
+    bi = engine.upload(W.indexed_for(engine, wl))
+    try:
+        got = np.asarray(bi.verify())
+    finally:
+        bi.free()
+    assert np.array_equal(got, wl.expected)
+    if name == "c4":
+        assert wl.n_invalid_jobs >= 1
