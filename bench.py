@@ -9,7 +9,8 @@ One process per GPU (torchrun for N>1; RANK/LOCAL_RANK/WORLD_SIZE from the env).
 verifies its own shard (weak scaling: sets shard across GPUs with no data-path collective; the
 optional --exchange flag adds the 576-byte Fp12 partial all-gather over RCCL and one final
 exponentiation).  A batch = B slots of gossip drained into one device batch
-(default 3); F batches are in flight per GPU (default 6, independent engines).  A step =
+(default 6); F batches are in flight per GPU (default 4, independent engines): ~66 ms per batch
+under load (profiles/r1_slots_sweep.txt).  A step =
 lb_batch_verify over one resident batch: all kernels + CSPRNG scalars + per-job result readback.
 Inputs are in HBM before the timed region.  Rank 0 prints one JSON line; value_distinct_roots is
 the same measurement with every signing root distinct (the no-sharing bound).
@@ -40,10 +41,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c3")
-    ap.add_argument("--slots", type=int, default=3,
+    ap.add_argument("--slots", type=int, default=6,
                     help="c3: slots of gossip drained into one device batch (profiles/r1_slots_sweep.txt)")
     ap.add_argument("--exchange", action="store_true", help="RCCL all-gather of Fp12 partials per step")
-    ap.add_argument("--inflight", type=int, default=6,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: independent engines (own streams + workspaces) driven by "
                          "one host thread each, like the reference pool's concurrent workers")
     ap.add_argument("--no-cpu-baseline", action="store_true")
