@@ -72,7 +72,8 @@ LB_NI jac<F> jac_dbl(jac<F> p) {
 }
 
 // add-2007-bl with the exceptional cases handled
-template <class F>
+// kInl = true keeps the exceptional doubling inline too (a kernel with no out-of-line calls).
+template <class F, bool kInl = false>
 LB_HD jac<F> jac_add_i(const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
@@ -85,7 +86,10 @@ LB_HD jac<F> jac_add_i(const jac<F>& p, const jac<F>& q) {
   F H = f_sub(U2, U1);
   F rr = f_dbl(f_sub(S2, S1));
   if (f_is_zero(H)) {
-    if (f_is_zero(rr)) return jac_dbl(p);
+    if (f_is_zero(rr)) {
+      if constexpr (kInl) return jac_dbl_i(p);
+      else return jac_dbl(p);
+    }
     return jac_infinity<F>();
   }
   F I = f_sqr(f_dbl(H));
@@ -104,7 +108,7 @@ LB_NI jac<F> jac_add(jac<F> p, jac<F> q) {
 }
 
 // madd-2007-bl: p Jacobian + q affine (q not infinity)
-template <class F>
+template <class F, bool kInl = false>
 LB_HD jac<F> jac_add_aff_i(const jac<F>& p, const aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.z);
@@ -113,7 +117,10 @@ LB_HD jac<F> jac_add_aff_i(const jac<F>& p, const aff<F>& q) {
   F H = f_sub(U2, p.x);
   F rr = f_dbl(f_sub(S2, p.y));
   if (f_is_zero(H)) {
-    if (f_is_zero(rr)) return jac_dbl(p);
+    if (f_is_zero(rr)) {
+      if constexpr (kInl) return jac_dbl_i(p);
+      else return jac_dbl(p);
+    }
     return jac_infinity<F>();
   }
   F HH = f_sqr(H);
@@ -171,8 +178,9 @@ LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
 // lanes follow one path.  Distinct words give distinct r (the lattice {(a, b): a + b lambda = 0
 // mod q} has no non-zero vector with |a|, |b| < 2^32), so a uniform non-zero word is a uniform
 // draw from 2^64 - 1 distinct blinding values, the set size behind blst's 64-bit randomness.
-template <class F>
-LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {
+// (jac_mul_glv_i is the inline body: k_pk_blind keeps the table in registers.)
+template <class F, bool kInl = false>
+LB_HD jac<F> jac_mul_glv_i(const aff<F>& t1, const aff<F>& t2, const aff<F>& t3, uint64_t w) {
   jac<F> acc = jac_infinity<F>();
   for (int i = 31; i >= 0; i--) {
     acc = jac_dbl_i(acc);
@@ -180,10 +188,14 @@ LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {
     aff<F> t;
     t.x = d == 1u ? t1.x : (d == 2u ? t2.x : t3.x);
     t.y = d == 1u ? t1.y : (d == 2u ? t2.y : t3.y);
-    jac<F> s = jac_add_aff_i(acc, t);
+    jac<F> s = jac_add_aff_i<F, kInl>(acc, t);
     if (d != 0u) acc = s;
   }
   return acc;
+}
+template <class F>
+LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {
+  return jac_mul_glv_i(t1, t2, t3, w);
 }
 
 // [k]P for a 64-bit scalar, P Jacobian (used after aggregation, before the one inversion)
@@ -241,6 +253,23 @@ LB_HD bool g2_in_subgroup(const g2j& p) {
   if (jac_is_inf(p)) return true;
   g2j xp = jac_neg(jac_mul_xabs(p));
   return jac_eq(g2_psi(p), xp);
+}
+
+// The same test for an affine point that is not infinity (a decoded signature, z = 1):
+// [|x|]P by mixed additions with the loop state in registers, and psi(P) kept affine, so the
+// comparison with [x]P = -acc is psi.x Z^2 == X and psi.y Z^3 == -Y.
+LB_HD bool g2_aff_in_subgroup_i(const g2a& a) {
+  g2j acc = jac_from_aff(a);
+  for (int i = 62; i >= 0; i--) {
+    acc = jac_dbl_i(acc);
+    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_aff_i(acc, a);
+  }
+  if (jac_is_inf(acc)) return false;  // psi(P) is finite
+  fp2 z2 = fp2_sqr(acc.z);
+  fp2 px = fp2_mul(fp2_conj(a.x), fp2_load(LB_PSI_CX));
+  if (!fp2_eq(fp2_mul(px, z2), acc.x)) return false;
+  fp2 py = fp2_mul(fp2_conj(a.y), fp2_load(LB_PSI_CY));
+  return fp2_eq(fp2_mul(fp2_mul(py, z2), acc.z), fp2_neg(acc.y));
 }
 
 // h_eff * P via psi (RFC 9380 App. G.3 / Budroni-Pintore)

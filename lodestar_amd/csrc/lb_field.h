@@ -394,8 +394,10 @@ LB_HD void lb_sub_in(uint32_t* a, const uint32_t* b) {
   uint32_t br = 0;
   LB_UNROLL for (int j = 0; j < 12; j++) a[j] = LB_SUBC(a[j], b[j], br, &br);
 }
-// plain a in [0, p) -> a^-1 mod p (plain), 0 -> 0
-LB_NI fp fp_inv_plain_vt(fp a) {
+// plain a in [0, p) -> a^-1 mod p (plain), 0 -> 0.  fp_inv_plain_vt_i is the inline body (a
+// kernel whose call graph is all inline keeps its own register budget), fp_inv_plain_vt the
+// out-of-line entry.
+LB_HD fp fp_inv_plain_vt_i(fp a) {
   if (fp_is_zero(a)) return a;
   uint32_t u[12], v[12];
   fp x1 = fp_zero(), x2 = fp_zero();
@@ -441,8 +443,10 @@ LB_NI fp fp_inv_plain_vt(fp a) {
     }
   }
 }
+LB_NI fp fp_inv_plain_vt(fp a) { return fp_inv_plain_vt_i(a); }
 // Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
 LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
+LB_HD fp fp_inv_i(const fp& a) { return fp_mul(fp_inv_plain_vt_i(a), fp_load(LB_R3)); }
 LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
 LB_HD fp fp_isqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_ISQRT, 378); }  // a^((p-3)/4)
 // Quadratic character by the binary Jacobi-symbol algorithm (variable time; every input is
@@ -568,7 +572,9 @@ LB_HD bool fp2_is_square(const fp2& a) { return fp_is_square(fp_add(fp_sqr(a.c0)
 
 // Square root in Fp2 by the complex method (p = 3 mod 4): three Fp exponentiations,
 // no data-dependent branches.  Returns true iff a is a square; `out` is some root.
-LB_NI bool fp2_sqrt(fp2& out, fp2 a) {
+// fp2_sqrt_i is the inline body (signature decoding keeps its point in registers), fp2_sqrt
+// the out-of-line entry.
+LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
   fp inv2 = fp_load(LB_INV2);
@@ -589,6 +595,7 @@ LB_NI bool fp2_sqrt(fp2& out, fp2 a) {
   out.c1 = fp_select(delta_qr, q, s);
   return fp2_eq(fp2_sqr(out), a);
 }
+LB_NI bool fp2_sqrt(fp2& out, fp2 a) { return fp2_sqrt_i(out, a); }
 
 // RFC 9380 sgn0 for Fp2 (on canonical values)
 LB_HD uint32_t fp2_sgn0(const fp2& a) {

@@ -21,6 +21,9 @@
 #ifndef LB_MINW
 #define LB_MINW 1  // min waves per SIMD (2 caps registers at 256 but spills: measured slower)
 #endif
+#ifndef LB_MINW_G1
+#define LB_MINW_G1 2  // G1 kernels: one Fp multiply per step, so a second wave hides its latency
+#endif
 
 template <class T>
 __device__ __forceinline__ T soa_ld(const uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
@@ -78,7 +81,8 @@ __device__ __forceinline__ fp fp_shfl_down(const fp& a, unsigned d) {
   LB_UNROLL for (int j = 0; j < 12; j++) r.v[j] = __shfl_down(a.v[j], d, 64);
   return r;
 }
-__device__ fp fp_inv_block(const fp& z) {
+template <bool kInl = false>
+__device__ __forceinline__ fp fp_inv_block(const fp& z) {
   constexpr int NW = LB_INV_TPB / 64;
   __shared__ uint32_t s_tot[NW][12];
   __shared__ uint32_t s_inv[12];
@@ -97,7 +101,8 @@ __device__ fp fp_inv_block(const fp& z) {
   if (wv == 0) {
     fp t = fp_load(s_tot[0]);
     for (int w = 1; w < NW; w++) t = fp_mul(t, fp_load(s_tot[w]));
-    t = fp_inv(t);
+    if constexpr (kInl) t = fp_inv_i(t);
+    else t = fp_inv(t);
     if (lane == 0) LB_UNROLL for (int j = 0; j < 12; j++) s_inv[j] = t.v[j];
   }
   __syncthreads();
@@ -131,7 +136,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, con
     uint8_t b[96];
     ld_bytes<96>(b, sigs + (size_t)96 * i);
     st = g2_decompress96(b, a, inf);
-    if (st == LB_OK && !inf && !g2_in_subgroup(jac_from_aff(a))) st = LB_POINT_NOT_IN_GROUP;
+    if (st == LB_OK && !inf && !g2_aff_in_subgroup_i(a)) st = LB_POINT_NOT_IN_GROUP;
   }
   soa_st(sig_aff, n, i, a);
   // array-of-structures copy (192 B per set) for the MSM's gathers: one point = 12 x 16 B
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
 // r * PK (Jacobian) for the per-root sums.  block of LB_INV_TPB threads (fp_inv_block)
-__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
                                                          const uint32_t* __restrict__ chunk_acc,
                                                          const int32_t* __restrict__ chunk_status,
                                                          const uint32_t* __restrict__ pk_off,
@@ -307,7 +312,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, ui
     g1j acc = jac_infinity<fp>();
     for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
       st = chunk_status[c];
-      if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
+      if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add_i<fp, true>(acc, soa_ld<g1j>(chunk_acc, nc, c));
     }
     if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
     rj = acc;
@@ -319,7 +324,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, ui
   const bool need = ok && !fp_eq(rj.z, one);
   g1a pk;
   if (__syncthreads_or(need)) {
-    const fp ai = fp_inv_block(need ? rj.z : one);
+    const fp ai = fp_inv_block<true>(need ? rj.z : one);
     const fp ai2 = fp_sqr(ai);
     pk.x = fp_mul(rj.x, ai2);
     pk.y = fp_mul(fp_mul(rj.y, ai2), ai);
@@ -331,7 +336,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_pk_blind(uint32_t n, ui
     // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
     const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
     const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
-    rj = jac_mul_glv(pk, t2, t3, scalars[i]);
+    rj = jac_mul_glv_i<fp, true>(pk, t2, t3, scalars[i]);
   } else {
     rj = jac_infinity<fp>();
   }
