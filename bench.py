@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--slots", type=int, default=6,
                     help="c3: slots of gossip drained into one device batch (profiles/r1_slots_sweep.txt)")
     ap.add_argument("--exchange", action="store_true", help="RCCL all-gather of Fp12 partials per step")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=6,
                     help="batches in flight per GPU: independent engines (own streams + workspaces) driven by "
                          "one host thread each, like the reference pool's concurrent workers")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -222,14 +222,18 @@ LB_NI jac<F> jac_mul_u256(aff<F> p, const uint32_t* k) {
 }
 
 // [|x|]P for the curve parameter |x| = 0xd201000000010000 (wave-uniform bits)
-template <class F>
-LB_NI jac<F> jac_mul_xabs(jac<F> p) {
+template <class F, bool kInl = false>
+LB_HD jac<F> jac_mul_xabs_i(const jac<F>& p) {
   jac<F> acc = p;  // top bit
   for (int i = 62; i >= 0; i--) {
     acc = jac_dbl_i(acc);
-    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_i(acc, p);
+    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_i<F, kInl>(acc, p);
   }
   return acc;
+}
+template <class F>
+LB_NI jac<F> jac_mul_xabs(jac<F> p) {
+  return jac_mul_xabs_i(p);
 }
 
 // ------------------------------------------------------------------ G2 endomorphism psi
@@ -262,7 +266,7 @@ LB_HD bool g2_aff_in_subgroup_i(const g2a& a) {
   g2j acc = jac_from_aff(a);
   for (int i = 62; i >= 0; i--) {
     acc = jac_dbl_i(acc);
-    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_aff_i(acc, a);
+    if ((LB_X_ABS >> i) & 1ull) acc = jac_add_aff_i<fp2, true>(acc, a);
   }
   if (jac_is_inf(acc)) return false;  // psi(P) is finite
   fp2 z2 = fp2_sqr(acc.z);

@@ -320,7 +320,7 @@ LB_HD fp lb_tab8(const fp* t, uint32_t k) {
     default: return t[7];
   }
 }
-LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) {
+LB_HD fp fp_pow_const_i(fp a, const uint32_t* e, int top_bit) {
   fp tab[8];
   tab[0] = a;
   const fp a2 = fp_sqr(a);
@@ -447,6 +447,7 @@ LB_NI fp fp_inv_plain_vt(fp a) { return fp_inv_plain_vt_i(a); }
 // Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
 LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
 LB_HD fp fp_inv_i(const fp& a) { return fp_mul(fp_inv_plain_vt_i(a), fp_load(LB_R3)); }
+LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) { return fp_pow_const_i(a, e, top_bit); }
 LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
 LB_HD fp fp_isqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_ISQRT, 378); }  // a^((p-3)/4)
 // Quadratic character by the binary Jacobi-symbol algorithm (variable time; every input is
@@ -574,9 +575,12 @@ LB_HD bool fp2_is_square(const fp2& a) { return fp_is_square(fp_add(fp_sqr(a.c0)
 // no data-dependent branches.  Returns true iff a is a square; `out` is some root.
 // fp2_sqrt_i is the inline body (signature decoding keeps its point in registers), fp2_sqrt
 // the out-of-line entry.
+template <bool kInl = false>
 LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
-  fp alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
+  fp alpha;
+  if constexpr (kInl) alpha = fp_pow_const_i(norm, LB_EXP_SQRT, 378);
+  else alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
   fp inv2 = fp_load(LB_INV2);
   fp d1 = fp_mul(fp_add(a.c0, alpha), inv2);
   fp d2 = fp_mul(fp_sub(a.c0, alpha), inv2);
@@ -584,7 +588,9 @@ LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   fp delta = fp_select(fp_is_zero(d1), d2, d1);
   // z = delta^((p-3)/4), s = delta z = delta^((p+1)/4), and s z = delta^((p-1)/2) = +-1, so
   // 1/s = +-z: the square root and the inverse it needs come from one exponentiation
-  fp z = fp_isqrt_cand(delta);
+  fp z;
+  if constexpr (kInl) z = fp_pow_const_i(delta, LB_EXP_ISQRT, 378);
+  else z = fp_isqrt_cand(delta);
   fp s = fp_mul(delta, z);
   bool delta_qr = fp_eq(fp_sqr(s), delta);
   // if delta is a residue: x0 = s, x1 = a1/(2s); else (s^2 = -delta) x0 = a1/(2s), x1 = s

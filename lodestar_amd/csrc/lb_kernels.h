@@ -21,6 +21,13 @@
 #ifndef LB_MINW
 #define LB_MINW 1  // min waves per SIMD (2 caps registers at 256 but spills: measured slower)
 #endif
+#ifndef LB_MINW_DEC
+#define LB_MINW_DEC 2  // k_decode_sigs (all-inline call graph, so its own bound holds): spills,
+                       // but half the register file lets another batch's kernels co-reside
+#endif
+#ifndef LB_MINW_MSM
+#define LB_MINW_MSM 1  // k_msm_chunks (2 spills; within noise under load)
+#endif
 #ifndef LB_MINW_G1
 #define LB_MINW_G1 2  // G1 kernels: one Fp multiply per step, so a second wave hides its latency
 #endif
@@ -117,7 +124,7 @@ __device__ __forceinline__ fp fp_inv_block(const fp& z) {
 
 // ---------------------------------------------------------------- signatures
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                         const uint32_t* __restrict__ sig_sizes,
                                                         uint32_t* __restrict__ sig_aff,
                                                         uint4* __restrict__ sig_aos,
@@ -577,7 +584,7 @@ __global__ void __launch_bounds__(LB_TPB) k_msm_scatter(uint32_t n, const uint64
 }
 // chunk c of a bucket: Jacobian sum of its member points (AoS affine signatures; bit 31 of a
 // member = the [lambda] image)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_chunks(const uint32_t* __restrict__ bch,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32_t* __restrict__ bch,
                                                        const uint32_t* __restrict__ chunk_beg,
                                                        const uint32_t* __restrict__ chunk_end,
                                                        const uint32_t* __restrict__ members,
@@ -601,7 +608,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_chunks(const uint32_t* 
       p.x = fp2_mul_fp(p.x, fp_load(LB_PSI2_CX));
       p.y = fp2_neg(fp2_mul_fp(p.y, fp_load(LB_PSI2_CY)));
     }
-    acc = jac_add_aff_i(acc, p);
+    acc = jac_add_aff_i<fp2, true>(acc, p);
   }
   soa_st(bacc, cap, c, acc);
 }

@@ -28,7 +28,7 @@ LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
   fp2 x{fp_to_mont(x0), fp_to_mont(x1)};
   fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), fp2_load(LB_B2));
   fp2 y;
-  if (!fp2_sqrt_i(y, rhs)) return LB_POINT_NOT_ON_CURVE;
+  if (!fp2_sqrt_i<true>(y, rhs)) return LB_POINT_NOT_ON_CURVE;
   bool want_large = (f & 0x20) != 0;
   if (fp2_lex_larger(y) != want_large) y = fp2_neg(y);
   out.x = x;
