@@ -28,6 +28,9 @@
 #ifndef LB_MINW_MSM
 #define LB_MINW_MSM 1  // k_msm_chunks (2 spills; within noise under load)
 #endif
+#ifndef LB_MINW_GSUM
+#define LB_MINW_GSUM 1  // k_gsum_chunks (all-inline)
+#endif
 #ifndef LB_MINW_G1
 #define LB_MINW_G1 2  // G1 kernels: one Fp multiply per step, so a second wave hides its latency
 #endif
@@ -691,7 +694,7 @@ __global__ void __launch_bounds__(LB_TPB) k_job_status(uint32_t n_jobs, const ui
 }
 
 // chunk c of a group: Jacobian sum of r_i PK_i over its live members -> gacc (stride n)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_gsum_chunks(uint32_t n, const uint32_t* __restrict__ n_u,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n, const uint32_t* __restrict__ n_u,
                                                         const uint32_t* __restrict__ gch,
                                                         const uint32_t* __restrict__ chunk_beg,
                                                         const uint32_t* __restrict__ chunk_end,
@@ -705,7 +708,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_gsum_chunks(uint32_t n, con
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t i = members[k];
     if (!set_live[i]) continue;
-    acc = jac_add_i(acc, soa_ld<g1j>(rpk, n, i));  // r*PK Jacobian (infinity handled)
+    acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));  // r*PK Jacobian (infinity handled)
   }
   soa_st(gacc, n, c, acc);
 }
