@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, cons
 
 // Same as k_pk_chunks over the resident pubkey table (affine Montgomery, g1a SoA with
 // table_cap elements).  table_flag[t] = (decode status << 1) | is_infinity.  idx = pk_indices.
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks_idx(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                           const uint32_t* __restrict__ idx,
                                                           const uint32_t* __restrict__ table, uint32_t table_cap,
                                                           const uint32_t* __restrict__ table_flag, uint32_t table_n,
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks_idx(uint32_t nc, 
       break;
     }
     if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
-    acc = jac_add_aff(acc, soa_ld<g1a>(table, table_cap, t));
+    acc = jac_add_aff_i<fp, true>(acc, soa_ld<g1a>(table, table_cap, t));
   }
   soa_st(chunk_acc, nc, c, acc);
   chunk_status[c] = st;
