@@ -34,7 +34,7 @@ unsigned long long cnt_decode(const uint8_t* sig96) {
   lb_count_mul = 0;
   g2a a; bool inf;
   int st = g2_decompress96(sig96, a, inf);
-  if (st == 0 && !inf) g2_in_subgroup(jac_from_aff(a));
+  if (st == 0 && !inf) g2_aff_in_subgroup_i(a);  // as k_decode_sigs
   return lb_count_mul;
 }
 unsigned long long cnt_hash_map(const uint8_t* msg, int which) {

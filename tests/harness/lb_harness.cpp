@@ -38,6 +38,7 @@ int h_map_to_curve(const uint8_t* u96, uint8_t* out192) { return wrg2(out192, ma
 int h_hash_to_g2(const uint8_t* msg, uint8_t* out192) { return wrg2(out192, hash_to_g2(msg)); }
 int h_g2_clear_cofactor(const uint8_t* p192, uint8_t* out192) { return wrg2(out192, g2_clear_cofactor(jac_from_aff(rdg2(p192)))); }
 int h_g2_in_subgroup(const uint8_t* p192) { return g2_in_subgroup(jac_from_aff(rdg2(p192))); }
+int h_g2_aff_in_subgroup(const uint8_t* p192) { return g2_aff_in_subgroup_i(rdg2(p192)); }
 int h_g2_psi(const uint8_t* p192, uint8_t* out192) { return wrg2(out192, g2_psi(jac_from_aff(rdg2(p192)))); }
 int h_g2_mul(const uint8_t* p192, uint64_t k, uint8_t* out192) { return wrg2(out192, jac_mul_u64(rdg2(p192), k)); }
 int h_g2_add(const uint8_t* p, const uint8_t* q, uint8_t* o) { return wrg2(o, jac_add(jac_from_aff(rdg2(p)), jac_from_aff(rdg2(q)))); }

@@ -133,6 +133,19 @@ def test_g2_subgroup_cofactor_psi(L):
     assert fg2(o192.raw) == o.g2_psi(q)
 
 
+def test_g2_aff_subgroup_matches_jacobian(L):
+    # k_decode_sigs runs the affine, mixed-addition form of the psi == [x] test; it must agree
+    # with the Jacobian form (and the oracle) on members and non-members of G2
+    rnd = random.Random(11)
+    for j in range(6):
+        msg = bytes(rnd.getrandbits(8) for _ in range(32))
+        H = o.hash_to_g2(msg)
+        q = o.iso_map(o.map_to_curve_sswu(o.hash_to_field_fp2(msg, 2, o.DST_POP)[j % 2]))
+        for P, want in ((H, 1), (q, 0), (o.g2_neg(q), 0), (o.g2_neg(H), 1)):
+            assert L.h_g2_aff_in_subgroup(g2b(P)) == want
+            assert L.h_g2_in_subgroup(g2b(P)) == want
+
+
 def test_group_law(L):
     rnd = random.Random(3)
     H = o.hash_to_g2(b"\x01" * 32)
