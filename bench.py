@@ -193,7 +193,7 @@ def main():
     if a.pubkey_bytes:
         batches = [e.upload(W.PackedJobs(job_off=wl.packed.job_off, pk_off=wl.packed.pk_off,
                                          pubkeys=wl.packed.pubkeys, msgs=wl.packed.msgs, sigs=wl.packed.sigs,
-                                         sig_sizes=None)) for e in engs]
+                                         sig_sizes=wl.packed.sig_sizes)) for e in engs]
     else:
         batches = [e.upload(W.indexed_for(e, wl)) for e in engs]
     batch = batches[0]

@@ -64,7 +64,14 @@ const char* lb_error_name(int32_t code);
 /* ABI version (bumped on incompatible changes). */
 int32_t lb_abi_version(void);
 
-/* One engine per GPU (one process per GPU in multi-GPU runs).  device < 0 = current. */
+/*
+ * One engine = one batch in flight on one GPU (own HIP streams and device workspaces); a process
+ * may drive several engines per GPU concurrently (the reference runs one job package per worker
+ * thread at a time, multithread/index.ts:290-381).  device < 0 = current.  Returns
+ * LB_ERR_DEVICE once the per-device engine cap is reached (7, or LB_MAX_ENGINES_PER_DEVICE):
+ * past it, a dispatch of the per-root kernels can fail to get private-segment scratch and the HSA
+ * queue aborts asynchronously (measured at 8 engines, profiles/r2_inflight8_abort.txt).
+ */
 int32_t lb_engine_create(int32_t device, lb_engine** out);
 void lb_engine_destroy(lb_engine* e);
 
@@ -113,11 +120,25 @@ int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* scalars, uin
                          int32_t* out_job);
 int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials576, uint32_t n, int32_t* ok);
 
-/* upload + verify + free in one call */
+/*
+ * Upload + verify in one call (the worker's verifyManySignatureSets, worker.ts:32-108): inputs go
+ * into an engine-owned device workspace that is grown once and reused (no per-call device
+ * allocation).  Inputs in pinned host memory (lb_host_alloc) are DMA'd directly; pageable inputs
+ * are staged by the HIP runtime.
+ */
 int32_t lb_verify_jobs(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
                        const uint32_t* set_pk_offsets, const uint8_t* pubkeys,
                        const uint8_t* signing_roots, const uint8_t* signatures,
                        const uint32_t* sig_sizes, const uint64_t* scalars, int32_t* out_job);
+/* lb_verify_jobs over the resident pubkey table (pk_indices as in lb_batch_create_indexed) */
+int32_t lb_verify_jobs_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                               const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
+                               const uint8_t* signing_roots, const uint8_t* signatures,
+                               const uint32_t* sig_sizes, const uint64_t* scalars, int32_t* out_job);
+
+/* Pinned (page-locked) host memory for request staging; NULL on failure. */
+void* lb_host_alloc(size_t bytes);
+void lb_host_free(void* p);
 
 /*
  * G1 pubkey aggregation (getAggregatedPubkey + toBytes(uncompressed)):
@@ -158,7 +179,8 @@ uint32_t lb_pubkey_table_size(const lb_engine* e);
 /*
  * Like lb_batch_create, but set i aggregates table entries pk_indices[set_pk_offsets[i] ..
  * set_pk_offsets[i+1]) instead of carrying pubkey bytes (4 bytes per key on the bus instead of 96).
- * An index beyond the table makes that set's job reject with LB_ERR_ARGUMENT.
+ * An index beyond the table makes that set's job reject with LB_ERR_ARGUMENT.  pk_indices may be
+ * NULL only when no set carries a key (set_pk_offsets[n_sets] == 0), else LB_ERR_ARGUMENT.
  */
 int32_t lb_batch_create_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
                                 const uint32_t* set_pk_offsets, const uint32_t* pk_indices,

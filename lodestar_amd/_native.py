@@ -55,6 +55,10 @@ SIGNATURES = {
     "lb_fp12_product_is_one": (ctypes.c_int32, [_vp, _u8p, ctypes.c_uint32, _i32p]),
     "lb_verify_jobs": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u32p, _u8p, _u8p, _u8p, _u32p, _u64p,
                                         _i32p]),
+    "lb_verify_jobs_indexed": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u32p, _u32p, _u8p, _u8p, _u32p,
+                                                _u64p, _i32p]),
+    "lb_host_alloc": (_vp, [ctypes.c_size_t]),
+    "lb_host_free": (None, [_vp]),
     "lb_aggregate_pubkeys": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u8p, _u8p, _i32p]),
     "lb_g1_decompress": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _i32p, ctypes.c_int32]),
     "lb_sk_to_pk": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),

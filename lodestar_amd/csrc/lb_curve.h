@@ -262,8 +262,93 @@ LB_HD bool g2_in_subgroup(const g2j& p) {
 // The same test for an affine point that is not infinity (a decoded signature, z = 1):
 // [|x|]P by mixed additions with the loop state in registers, and psi(P) kept affine, so the
 // comparison with [x]P = -acc is psi.x Z^2 == X and psi.y Z^3 == -Y.
+// Register-lean forms for the two-waves-per-SIMD signature kernels (256 VGPRs).  kInl = true
+// inlines the Fp products (fp_mul28 / fp_sqr28): with out-of-line products every value live
+// across a call must sit in the ~100 callee-saved VGPRs of the AMDGPU calling convention, which
+// the G2 ladder's state overflows.  The statement order is the live-range order: each temporary
+// dies as early as the formula allows (dbl-2009-l and madd-2007-bl, reordered; same results as
+// jac_dbl_i / jac_add_aff_i).
+// (inline products are fenced with scheduling barriers: interleaving the three independent
+// products of an Fp2 multiplication would hold three 28-column accumulators at once)
+template <bool kInl>
+LB_HD fp lean_mul(const fp& a, const fp& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kInl) {
+    __builtin_amdgcn_sched_barrier(0);
+    fp r = fp_mul28(a, b);
+    __builtin_amdgcn_sched_barrier(0);
+    return r;
+  }
+#endif
+  return fp_mul(a, b);
+}
+template <bool kInl>
+LB_HD fp lean_sqr(const fp& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kInl) {
+    __builtin_amdgcn_sched_barrier(0);
+    fp r = fp_sqr28(a);
+    __builtin_amdgcn_sched_barrier(0);
+    return r;
+  }
+#endif
+  return fp_sqr(a);
+}
+template <bool kInl>
+LB_HD fp2 lean2_mul(const fp2& a, const fp2& b) {
+  fp t0 = lean_mul<kInl>(a.c0, b.c0);
+  fp t1 = lean_mul<kInl>(a.c1, b.c1);
+  fp t2 = lean_mul<kInl>(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+template <bool kInl>
+LB_HD fp2 lean2_sqr(const fp2& a) {
+  fp t0 = lean_mul<kInl>(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp t1 = lean_mul<kInl>(a.c0, a.c1);
+  return fp2{t0, fp_dbl(t1)};
+}
+template <bool kInl>
+LB_HD void g2_dbl_lean(g2j& p) {
+  p.z = fp2_dbl(lean2_mul<kInl>(p.y, p.z));        // Z3 = 2 Y Z (Z dead)
+  fp2 B = lean2_sqr<kInl>(p.y);                    // Y dead from here on
+  fp2 C = lean2_sqr<kInl>(B);
+  fp2 A = lean2_sqr<kInl>(p.x);
+  fp2 D = lean2_sqr<kInl>(fp2_add(p.x, B));        // X, B dead
+  D = fp2_dbl(fp2_sub(fp2_sub(D, A), C));
+  fp2 E = fp2_mul3(A);                             // A dead
+  p.x = fp2_sub(lean2_sqr<kInl>(E), fp2_dbl(D));   // X3
+  p.y = fp2_sub(lean2_mul<kInl>(E, fp2_sub(D, p.x)), fp2_mul8(C));
+}
+// p + q for q affine, p finite (the exceptional cases P == +-Q are handled)
+template <bool kInl>
+LB_HD void g2_add_aff_lean(g2j& p, const g2a& q) {
+  fp2 Z1Z1 = lean2_sqr<kInl>(p.z);
+  fp2 H = fp2_sub(lean2_mul<kInl>(q.x, Z1Z1), p.x);    // U2 - X1
+  fp2 rr = lean2_mul<kInl>(lean2_mul<kInl>(q.y, p.z), Z1Z1);   // S2
+  rr = fp2_dbl(fp2_sub(rr, p.y));
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(rr)) {
+      g2_dbl_lean<kInl>(p);
+    } else {
+      p = jac_infinity<fp2>();
+    }
+    return;
+  }
+  fp2 HH = lean2_sqr<kInl>(H);
+  p.z = fp2_sub(fp2_sub(lean2_sqr<kInl>(fp2_add(p.z, H)), Z1Z1), HH);  // Z, Z1Z1 dead
+  fp2 I = fp2_mul4(HH);                                                  // HH dead
+  fp2 J = lean2_mul<kInl>(H, I);                                         // H dead
+  fp2 V = lean2_mul<kInl>(p.x, I);                                       // X, I dead
+  fp2 YJ = fp2_dbl(lean2_mul<kInl>(p.y, J));                             // Y dead
+  p.x = fp2_sub(fp2_sub(lean2_sqr<kInl>(rr), J), fp2_dbl(V));           // J dead
+  p.y = fp2_sub(lean2_mul<kInl>(rr, fp2_sub(V, p.x)), YJ);
+}
+
+// The loop is kept rolled, and the base point is re-read from memory (`src`, the caller's
+// copy) at the five additions instead of being held across the 63 doublings.
 LB_HD bool g2_aff_in_subgroup_i(const g2a& a) {
   g2j acc = jac_from_aff(a);
+#pragma clang loop unroll(disable)
   for (int i = 62; i >= 0; i--) {
     acc = jac_dbl_i(acc);
     if ((LB_X_ABS >> i) & 1ull) acc = jac_add_aff_i<fp2, true>(acc, a);

@@ -75,6 +75,7 @@ const char* const kStageNames[kStages] = {"decode_sigs", "dedup",   "hash_map", 
 struct lb_batch {
   uint32_t n_jobs = 0, n_sets = 0, n_pks = 0;
   std::vector<uint32_t> job_off;  // host copy (bisection bookkeeping)
+  std::vector<uint32_t> h_set_chunk_off, h_chunk_lo;  // host staging of the chunk decomposition
   uint32_t n_chunks = 0;           // pubkey aggregation chunks (k_pk_chunks)
   bool indexed = false;            // pubkeys are indices into the engine's resident table
   dbuf d_job_off, d_pk_off, d_pks, d_msgs, d_sigs, d_sig_sizes, d_set_chunk_off, d_chunk_lo;
@@ -116,7 +117,23 @@ struct lb_engine {
   hipEvent_t ev0[kStages] = {}, ev1[kStages] = {};
   bool used[kStages] = {};
   float last_ms[kStages] = {};
+  // pinned host word for the distinct-root count read back after grouping: the per-root kernels
+  // are launched over that count, not over the set count (their scratch is sized per dispatch)
+  uint32_t* h_nu = nullptr;
+  // engine-owned input workspace reused by lb_verify_jobs* (no per-call device allocation)
+  lb_batch* scratch = nullptr;
 };
+
+// Engines per device are capped so that one process cannot create more concurrently active
+// HIP streams than the device can back with queues and scratch (exhaustion aborts the HSA queue
+// asynchronously instead of returning an error).  LB_MAX_ENGINES_PER_DEVICE overrides the cap.
+static std::mutex g_engine_mu;
+static int g_engine_count[64];
+static int max_engines_per_device() {
+  const char* v = getenv("LB_MAX_ENGINES_PER_DEVICE");
+  int k = v ? atoi(v) : 0;
+  return k > 0 ? k : 7;
+}
 
 #define LB_HIP(call)                                                                        \
   do {                                                                                      \
@@ -190,13 +207,28 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
     return LB_ERR_NO_DEVICE;
   }
   LB_HIP(hipSetDevice(device));
+  if (device >= 64) return LB_ERR_NO_DEVICE;
+  {
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    if (g_engine_count[device] >= max_engines_per_device()) {
+      fprintf(stderr, "lodestar_bls: engine limit (%d per device) reached on device %d\n", max_engines_per_device(),
+              device);
+      return LB_ERR_DEVICE;
+    }
+    g_engine_count[device]++;
+  }
   lb_engine* e = new lb_engine();
   e->device = device;
   while (getrandom(&e->msg_key, 8, 0) != 8) {
   }
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess) {
+    if (e->stream) hipStreamDestroy(e->stream);
+    if (e->stream2) hipStreamDestroy(e->stream2);
     delete e;
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    g_engine_count[device]--;
     return LB_ERR_DEVICE;
   }
   hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming);
@@ -232,8 +264,14 @@ void lb_engine_destroy(lb_engine* e) {
   hipEventDestroy(e->ev_fork);
   hipEventDestroy(e->ev_dec);
   hipStreamSynchronize(e->stream2);
+  if (e->scratch) delete e->scratch;
+  if (e->h_nu) hipHostFree(e->h_nu);
   hipStreamDestroy(e->stream2);
   hipStreamDestroy(e->stream);
+  {
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    g_engine_count[e->device]--;
+  }
   delete e;
 }
 
@@ -256,24 +294,24 @@ int32_t lb_engine_last_profile(lb_engine* e, const char** names, float* ms, int3
 
 }  // extern "C"
 
-static int32_t batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets,
-                            const uint8_t* pubkeys, const uint32_t* pk_indices, const uint8_t* signing_roots,
-                            const uint8_t* signatures, const uint32_t* sig_sizes, lb_batch** out) {
-  if (!e || !out || !job_offsets || !set_pk_offsets) return LB_ERR_ARGUMENT;
-  *out = nullptr;
+// Validates the offsets and uploads one batch into b's device buffers (grown, never shrunk, so
+// an engine-owned workspace batch is reused across calls without device allocation).  The caller
+// holds e->mu.
+static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint32_t* job_offsets,
+                          const uint32_t* set_pk_offsets, const uint8_t* pubkeys, const uint32_t* pk_indices,
+                          const uint8_t* signing_roots, const uint8_t* signatures, const uint32_t* sig_sizes) {
+  if (!e || !job_offsets || !set_pk_offsets) return LB_ERR_ARGUMENT;
   if (job_offsets[0] != 0) return LB_ERR_ARGUMENT;
   for (uint32_t j = 0; j < n_jobs; j++)
     if (job_offsets[j + 1] < job_offsets[j]) return LB_ERR_ARGUMENT;
-  uint32_t n_sets = job_offsets[n_jobs];
+  const uint32_t n_sets = job_offsets[n_jobs];
   if (set_pk_offsets[0] != 0) return LB_ERR_ARGUMENT;
   for (uint32_t i = 0; i < n_sets; i++)
     if (set_pk_offsets[i + 1] < set_pk_offsets[i]) return LB_ERR_ARGUMENT;
-  uint32_t n_pks = set_pk_offsets[n_sets];
+  const uint32_t n_pks = set_pk_offsets[n_sets];
   const bool indexed = pk_indices != nullptr;
   if ((n_sets && (!signing_roots || !signatures)) || (n_pks && !pubkeys && !indexed)) return LB_ERR_ARGUMENT;
-  std::lock_guard<std::mutex> lk(e->mu);
   LB_HIP(hipSetDevice(e->device));
-  lb_batch* b = new lb_batch();
   b->device = e->device;
   b->n_jobs = n_jobs;
   b->n_sets = n_sets;
@@ -286,7 +324,10 @@ static int32_t batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_o
     return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, e->stream);
   };
   // chunk decomposition of every set's pubkey range (<= LB_PK_CHUNK keys per chunk)
-  std::vector<uint32_t> set_chunk_off(n_sets + 1), chunk_lo;
+  std::vector<uint32_t>& set_chunk_off = b->h_set_chunk_off;
+  std::vector<uint32_t>& chunk_lo = b->h_chunk_lo;
+  set_chunk_off.resize(n_sets + 1);
+  chunk_lo.clear();
   for (uint32_t i = 0; i < n_sets; i++) {
     set_chunk_off[i] = (uint32_t)chunk_lo.size();
     for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK) chunk_lo.push_back(k);
@@ -307,11 +348,34 @@ static int32_t batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_o
   if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
   if (r != hipSuccess) {
     fprintf(stderr, "lodestar_bls: batch upload failed: %s\n", hipGetErrorString(r));
-    delete b;
     return LB_ERR_DEVICE;
+  }
+  return LB_OK;
+}
+
+static int32_t batch_create(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets,
+                            const uint8_t* pubkeys, const uint32_t* pk_indices, const uint8_t* signing_roots,
+                            const uint8_t* signatures, const uint32_t* sig_sizes, lb_batch** out) {
+  if (!e || !out) return LB_ERR_ARGUMENT;
+  *out = nullptr;
+  std::lock_guard<std::mutex> lk(e->mu);
+  lb_batch* b = new lb_batch();
+  int32_t st = batch_fill(e, b, n_jobs, job_offsets, set_pk_offsets, pubkeys, pk_indices, signing_roots, signatures,
+                          sig_sizes);
+  if (st != LB_OK) {
+    delete b;
+    return st;
   }
   *out = b;
   return LB_OK;
+}
+
+// pk_indices == NULL is only meaningful when no set carries a key (every set then rejects with
+// EMPTY_AGGREGATE_ARRAY); it is passed on as a one-word sentinel, never read.
+static const uint32_t kNoIndices[1] = {0};
+static int32_t check_null_indices(uint32_t n_jobs, const uint32_t* job_offsets, const uint32_t* set_pk_offsets) {
+  if (!job_offsets || !set_pk_offsets) return LB_ERR_ARGUMENT;
+  return set_pk_offsets[job_offsets[n_jobs]] == 0 ? LB_OK : LB_ERR_ARGUMENT;
 }
 
 extern "C" {
@@ -327,13 +391,23 @@ int32_t lb_batch_create_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* j
                                 const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
                                 const uint8_t* signing_roots, const uint8_t* signatures, const uint32_t* sig_sizes,
                                 lb_batch** out) {
-  if (!pk_indices && set_pk_offsets && job_offsets) {
-    // no keys at all is only valid when every set is empty
-    return batch_create(e, n_jobs, job_offsets, set_pk_offsets, nullptr, reinterpret_cast<const uint32_t*>(""),
-                        signing_roots, signatures, sig_sizes, out);
+  if (!pk_indices) {
+    const int32_t st = check_null_indices(n_jobs, job_offsets, set_pk_offsets);
+    if (st != LB_OK) return st;
+    pk_indices = kNoIndices;
   }
   return batch_create(e, n_jobs, job_offsets, set_pk_offsets, nullptr, pk_indices, signing_roots, signatures,
                       sig_sizes, out);
+}
+
+void* lb_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void lb_host_free(void* p) {
+  if (p) hipHostFree(p);
 }
 
 uint32_t lb_pubkey_table_size(const lb_engine* e) { return e ? e->table_n : 0; }
@@ -500,9 +574,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // signatures: decoded while s1 groups and hashes the messages
     {
       stage_scope sc(e, ST_DECODE, s2);
-      hipLaunchKernelGGL(k_decode_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
+      hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
                          b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
       hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s2, nj, b->d_job_off.as<uint32_t>(),
                          e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
                          e->set_live.as<uint32_t>());
@@ -524,16 +600,24 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
+      // distinct-root count to the host: the per-root kernels below are launched over it (a
+      // launch over the set count would size their private-segment scratch for n lanes)
+      LB_HIP(hipMemcpyAsync(e->h_nu, e->n_u.p, 4, hipMemcpyDeviceToHost, s1));
+      LB_HIP(hipStreamSynchronize(s1));
     }
+    const uint32_t nuh = *e->h_nu;
+    if (nuh == 0 || nuh > n) return LB_ERR_DEVICE;
+    mu = 1;
+    while (mu < nuh) mu <<= 1;
     // ---- s1: hash_to_G2 once per distinct root
     {
       stage_scope sc(e, ST_HASH_MAP, s1);
-      hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * n)), dim3(LB_TPB), 0, s1, n, nu, e->uniq_set.as<uint32_t>(),
+      hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * nuh)), dim3(LB_TPB), 0, s1, n, nuh, e->uniq_set.as<uint32_t>(),
                          b->d_msgs.as<uint8_t>(), e->q.as<uint32_t>());
     }
     {
       stage_scope sc(e, ST_HASH_FIN, s1);
-      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
+      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
                          e->h_aff.as<uint32_t>());
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
@@ -561,15 +645,16 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
     {
       stage_scope sc(e, ST_GSUM, s1);
-      hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+      // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
+      hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nuh + n / LB_GROUP_CHUNK)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(),
                          e->set_live.as<uint32_t>(), e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
-      hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+      hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
     }
     {
       stage_scope sc(e, ST_MILLER, s1);
-      hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+      hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                          e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
     }
     {
@@ -655,9 +740,8 @@ static void finish_profile(lb_engine* e) {
   }
 }
 
-extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* scalars, int32_t* out_job) {
-  if (!e || !b || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
-  std::lock_guard<std::mutex> lk(e->mu);
+// caller holds e->mu
+static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars, int32_t* out_job) {
   LB_HIP(hipSetDevice(e->device));
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
@@ -742,6 +826,12 @@ extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* sc
   return LB_OK;
 }
 
+extern "C" int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* scalars, int32_t* out_job) {
+  if (!e || !b || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(e->mu);
+  return verify_locked(e, b, scalars, out_job);
+}
+
 extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint8_t* out576,
                                     int32_t* out_job) {
   if (!e || !b || !out576 || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
@@ -786,17 +876,39 @@ extern "C" int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials5
   return LB_OK;
 }
 
+// upload into the engine-owned workspace batch + verify, under one hold of the engine lock
+static int32_t verify_jobs_ws(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                              const uint32_t* set_pk_offsets, const uint8_t* pubkeys, const uint32_t* pk_indices,
+                              const uint8_t* signing_roots, const uint8_t* signatures, const uint32_t* sig_sizes,
+                              const uint64_t* scalars, int32_t* out_job) {
+  if (!e || !job_offsets || (n_jobs && !out_job)) return LB_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!e->scratch) e->scratch = new lb_batch();
+  int32_t st = batch_fill(e, e->scratch, n_jobs, job_offsets, set_pk_offsets, pubkeys, pk_indices, signing_roots,
+                          signatures, sig_sizes);
+  if (st != LB_OK) return st;
+  return verify_locked(e, e->scratch, scalars, out_job);
+}
+
 extern "C" int32_t lb_verify_jobs(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
                                   const uint32_t* set_pk_offsets, const uint8_t* pubkeys,
                                   const uint8_t* signing_roots, const uint8_t* signatures,
                                   const uint32_t* sig_sizes, const uint64_t* scalars, int32_t* out_job) {
-  lb_batch* b = nullptr;
-  int32_t st = lb_batch_create(e, n_jobs, job_offsets, set_pk_offsets, pubkeys, signing_roots, signatures,
-                               sig_sizes, &b);
-  if (st != LB_OK) return st;
-  st = lb_batch_verify(e, b, scalars, out_job);
-  lb_batch_destroy(b);
-  return st;
+  return verify_jobs_ws(e, n_jobs, job_offsets, set_pk_offsets, pubkeys, nullptr, signing_roots, signatures,
+                        sig_sizes, scalars, out_job);
+}
+
+extern "C" int32_t lb_verify_jobs_indexed(lb_engine* e, uint32_t n_jobs, const uint32_t* job_offsets,
+                                          const uint32_t* set_pk_offsets, const uint32_t* pk_indices,
+                                          const uint8_t* signing_roots, const uint8_t* signatures,
+                                          const uint32_t* sig_sizes, const uint64_t* scalars, int32_t* out_job) {
+  if (!pk_indices) {
+    const int32_t st = check_null_indices(n_jobs, job_offsets, set_pk_offsets);
+    if (st != LB_OK) return st;
+    pk_indices = kNoIndices;
+  }
+  return verify_jobs_ws(e, n_jobs, job_offsets, set_pk_offsets, nullptr, pk_indices, signing_roots, signatures,
+                        sig_sizes, scalars, out_job);
 }
 
 extern "C" int32_t lb_aggregate_pubkeys(lb_engine* e, uint32_t n_sets, const uint32_t* set_pk_offsets,

@@ -25,6 +25,12 @@
 #define LB_MINW_DEC 2  // k_decode_sigs (all-inline call graph, so its own bound holds): spills,
                        // but half the register file lets another batch's kernels co-reside
 #endif
+#ifndef LB_MINW_SUB
+#define LB_MINW_SUB LB_MINW_DEC  // k_sig_subgroup
+#endif
+#ifndef LB_SUBGROUP_INL
+#define LB_SUBGROUP_INL true  // k_sig_subgroup: Fp products inline (no call-boundary spills)
+#endif
 #ifndef LB_MINW_MSM
 #define LB_MINW_MSM 1  // k_msm_chunks (2 spills; within noise under load)
 #endif
@@ -126,13 +132,19 @@ __device__ __forceinline__ fp fp_inv_block(const fp& z) {
 }
 
 // ---------------------------------------------------------------- signatures
+// Signature.fromBytes(sig, affine, validate=true) in two kernels, each small enough to run at two
+// waves per SIMD without register spills (one kernel doing both spilled ~2.2 KB per lane, i.e.
+// ~1.3 GB of scratch traffic per 116k-set launch, and its per-dispatch scratch grant exhausted
+// the runtime's pool at 8 batches in flight):
+//   k_decompress_sigs  ZCash decode + Fp2 square root  -> affine point (SoA + AoS), status
+//   k_sig_subgroup     Scott's psi check on the decoded points whose status is still OK
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decode_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
-                                                        const uint32_t* __restrict__ sig_sizes,
-                                                        uint32_t* __restrict__ sig_aff,
-                                                        uint4* __restrict__ sig_aos,
-                                                        uint32_t* __restrict__ sig_inf,
-                                                        int32_t* __restrict__ sig_status) {
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decompress_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                            const uint32_t* __restrict__ sig_sizes,
+                                                            uint32_t* __restrict__ sig_aff,
+                                                            uint4* __restrict__ sig_aos,
+                                                            uint32_t* __restrict__ sig_inf,
+                                                            int32_t* __restrict__ sig_status) {
   uint32_t i = lb_tid();
   if (i >= n) return;
   int st = LB_OK;
@@ -146,7 +158,6 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decode_sigs(uint32_t n,
     uint8_t b[96];
     ld_bytes<96>(b, sigs + (size_t)96 * i);
     st = g2_decompress96(b, a, inf);
-    if (st == LB_OK && !inf && !g2_aff_in_subgroup_i(a)) st = LB_POINT_NOT_IN_GROUP;
   }
   soa_st(sig_aff, n, i, a);
   // array-of-structures copy (192 B per set) for the MSM's gathers: one point = 12 x 16 B
@@ -156,17 +167,51 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decode_sigs(uint32_t n,
   sig_status[i] = st;
 }
 
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                         const uint32_t* __restrict__ sig_inf,
+                                                         int32_t* __restrict__ sig_status) {
+  uint32_t i = lb_tid();
+  if (i >= n) return;
+  if (sig_status[i] != LB_OK || sig_inf[i]) return;
+  // Scott's test psi(P) == [x]P with [|x|]P by the register-lean ladder (lb_curve.h); P is
+  // re-read from memory at the five additions rather than held across the doublings
+  const volatile uint32_t* vp = sig_aff;
+  auto load_p = [&]() {
+    g2a a;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&a);
+    LB_UNROLL for (int k = 0; k < 48; k++) w[k] = vp[(size_t)k * n + i];
+    return a;
+  };
+  g2j acc = jac_from_aff(load_p());
+#pragma clang loop unroll(disable)
+  for (int b = 62; b >= 0; b--) {
+    g2_dbl_lean<LB_SUBGROUP_INL>(acc);
+    if ((LB_X_ABS >> b) & 1ull) g2_add_aff_lean<LB_SUBGROUP_INL>(acc, load_p());
+  }
+  bool ok = !jac_is_inf(acc);  // psi(P) is finite
+  if (ok) {
+    const g2a a = load_p();
+    const fp2 z2 = fp2_sqr(acc.z);
+    ok = fp2_eq(fp2_mul(fp2_mul(fp2_conj(a.x), fp2_load(LB_PSI_CX)), z2), acc.x);
+    if (ok) {
+      const fp2 py = fp2_mul(fp2_conj(a.y), fp2_load(LB_PSI_CY));
+      ok = fp2_eq(fp2_mul(fp2_mul(py, z2), acc.z), fp2_neg(acc.y));
+    }
+  }
+  if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
+}
+
 // ---------------------------------------------------------------- hash_to_G2
-// Hashing runs once per DISTINCT signing root (k_msg_insert below): thread t handles unique
-// message t % n, field element u_{t / n}, for t % n < *n_u; output Jacobian points q (stride 2n).
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const uint32_t* __restrict__ n_u,
+// Hashing runs once per DISTINCT signing root (k_msg_insert below): launched over 2 nu threads
+// (nu = distinct roots, read back by the host); thread t handles unique message t % nu, field
+// element u_{t / nu}; output Jacobian points q (stride 2n: u_0 of root u at u, u_1 at n + u).
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32_t nu,
                                                      const uint32_t* __restrict__ uniq_set,
                                                      const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
-  uint32_t t = lb_tid();
-  if (t >= 2 * n) return;
-  uint32_t u = t < n ? t : t - n;
-  if (u >= *n_u) return;
-  uint32_t which = t < n ? 0u : 1u;
+  const uint32_t t = lb_tid();
+  if (t >= 2 * nu) return;
+  const uint32_t which = t < nu ? 0u : 1u;
+  const uint32_t u = which ? t - nu : t;
   uint8_t m[32];
   ld_bytes<32>(m, msgs + (size_t)32 * uniq_set[u]);
   uint32_t ub[64];
@@ -174,7 +219,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, const 
   const uint32_t* w = ub + 32 * which;
   fp2 u2{fp_from_be64_words(w), fp_from_be64_words(w + 16)};
   g2j p = map_to_curve_g2(u2);
-  soa_st(q, 2 * n, t, p);
+  soa_st(q, 2 * n, which * n + u, p);
 }
 
 // block of LB_INV_TPB threads (fp_inv_block)

@@ -182,23 +182,37 @@ class Engine:
 
     def verify_jobs(self, jobs, scalars: Optional[np.ndarray] = None) -> List[int]:
         """Per-job 1 / 0 / -code."""
-        b = self.upload(jobs)
-        try:
-            return [int(x) for x in b.verify(scalars)]
-        finally:
-            b.free()
+        return self.verify_jobs_packed(pack_jobs(jobs), scalars)
+
+    def verify_jobs_packed(self, packed: PackedJobs, scalars: Optional[np.ndarray] = None) -> List[int]:
+        """Upload + verify through the engine-owned workspace (lb_verify_jobs[_indexed]): the
+        drop-in path, no per-call device allocation."""
+        out = np.zeros(max(packed.n_jobs, 1), dtype=np.int32)
+        sc = None if scalars is None else np.ascontiguousarray(scalars, dtype=np.uint64)
+        if packed.pk_indices is not None:
+            idx = np.ascontiguousarray(packed.pk_indices, dtype=np.uint32)
+            st = self.lib.lb_verify_jobs_indexed(
+                self.h, packed.n_jobs, _p(packed.job_off, ctypes.c_uint32), _p(packed.pk_off, ctypes.c_uint32),
+                _p(idx if idx.size else None, ctypes.c_uint32), _p(packed.msgs, ctypes.c_uint8),
+                _p(packed.sigs, ctypes.c_uint8), _p(packed.sig_sizes, ctypes.c_uint32), _p(sc, ctypes.c_uint64),
+                _p(out, ctypes.c_int32))
+        else:
+            st = self.lib.lb_verify_jobs(
+                self.h, packed.n_jobs, _p(packed.job_off, ctypes.c_uint32), _p(packed.pk_off, ctypes.c_uint32),
+                _p(packed.pubkeys, ctypes.c_uint8), _p(packed.msgs, ctypes.c_uint8), _p(packed.sigs, ctypes.c_uint8),
+                _p(packed.sig_sizes, ctypes.c_uint32), _p(sc, ctypes.c_uint64), _p(out, ctypes.c_int32))
+        _check(st)
+        return [int(x) for x in out[: packed.n_jobs]]
 
     def verify_jobs_indexed(self, jobs, indices, scalars: Optional[np.ndarray] = None) -> List[int]:
         """Jobs whose pubkeys are table indices: indices[j][s] = list of table indices of set s."""
-        packed = pack_jobs([[SetInput([bytes(96)] * len(ix), s.signing_root, s.signature)
-                             for s, ix in zip(job, jix)] for job, jix in zip(jobs, indices)])
+        packed = pack_jobs([[SetInput([], s.signing_root, s.signature) for s in job] for job in jobs])
+        counts = [len(ix) for jix in indices for ix in jix]
+        packed.pk_off = np.zeros(len(counts) + 1, dtype=np.uint32)
+        packed.pk_off[1:] = np.cumsum(counts, dtype=np.uint64).astype(np.uint32)
         packed.pubkeys = None
         packed.pk_indices = np.asarray([i for jix in indices for ix in jix for i in ix], dtype=np.uint32)
-        b = Batch(self, packed)
-        try:
-            return [int(x) for x in b.verify(scalars)]
-        finally:
-            b.free()
+        return self.verify_jobs_packed(packed, scalars)
 
     def product_is_one(self, partials: Sequence[bytes]) -> bool:
         buf = np.frombuffer(b"".join(partials), dtype=np.uint8).copy() if partials else np.zeros(1, np.uint8)

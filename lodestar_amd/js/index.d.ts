@@ -2,7 +2,7 @@
 // Mirrors packages/beacon-node/src/chain/bls/interface.ts:3-46 and
 // packages/state-transition/src/util/signatureSets.ts:5-22.
 
-export type PublicKeyLike = Uint8Array | {toBytes(): Uint8Array};
+export type PublicKeyLike = Uint8Array | GpuPublicKey | {toBytes(): Uint8Array};
 
 export declare const SignatureSetType: {single: "single"; aggregate: "aggregate"};
 
@@ -24,10 +24,20 @@ export declare class QueueError extends Error {
   type: {code: string};
 }
 
+/** A key registered in the GPU-resident table (the epoch cache's index2pubkey entry). */
+export declare class GpuPublicKey {
+  readonly index: number;
+  toBytes(): Uint8Array;
+}
+
 export declare class BlsGpuVerifier implements IBlsVerifier {
-  constructor(opts?: {device?: number; blsVerifyAllMultiThread?: boolean});
+  /** engines: batches in flight on the device (default 2), each with its own streams + workspace */
+  constructor(opts?: {device?: number; engines?: number; blsVerifyAllMultiThread?: boolean});
+  /** 48- or 96-byte keys -> handles carrying their table index (validate: keyValidate checks) */
+  registerPubkeys(keys: Uint8Array[], validate?: boolean): GpuPublicKey[];
   verifySignatureSets(sets: ISignatureSet[], opts?: VerifySignatureOpts): Promise<boolean>;
   close(): Promise<void>;
+  readonly stats: {batches: number; jobs: number; sets: number; jobsInvalid: number; jobsError: number};
 }
 
 export declare function chunkifyMaximizeChunkSize<T>(arr: T[], minPerChunk: number): T[][];

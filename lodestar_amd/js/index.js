@@ -10,12 +10,21 @@
  *   - each job resolves true / false or rejects with the blst error string, independently of the
  *     other jobs in the same GPU batch (multithread.test.ts:86-103);
  *   - close() rejects queued jobs with QUEUE_ABORTED (:176-197).
- * Instead of worker threads, one runner hands every queued job to the GPU as ONE batch through the
- * N-API addon (../napi/lb_napi.c -> include/lodestar_bls.h); the event loop is never blocked.
+ * Instead of worker threads, `engines` GPU engines (default 2; each one batch in flight with its own
+ * HIP streams and device workspace) take packages from one queue: an idle engine drains EVERY
+ * queued job into one device batch through the N-API addon (../napi/lb_napi.c ->
+ * include/lodestar_bls.h), like the reference's idle worker taking the next package
+ * (multithread/index.ts:290-330).  The event loop is never blocked.
  *
- * Public keys: a `PublicKey` here is anything with `toBytes()` returning the 96-byte uncompressed
- * encoding (what the reference main thread sends to workers: getAggregatedPubkey(s).toBytes(
- * PointFormat.uncompressed), multithread/index.ts:160), or a 96-byte Uint8Array.
+ * Public keys: a `PublicKey` here is
+ *   - a handle returned by registerPubkeys() (the epoch cache's index2pubkey entries,
+ *     state-transition/src/cache/pubkeyCache.ts:56-77): it carries its index into the
+ *     GPU-resident key table, and packages whose keys all have one ship 4-byte indices;
+ *   - or anything with `toBytes()` returning the 96-byte uncompressed encoding (what the reference
+ *     main thread sends to workers: getAggregatedPubkey(s).toBytes(PointFormat.uncompressed),
+ *     multithread/index.ts:160), or a 96-byte Uint8Array.
+ * Malformed inputs (root not 32 bytes, pubkey not 96 bytes, signature not a Uint8Array) reject
+ * only the call that carries them, before anything is queued.
  */
 const path = require("path");
 
@@ -46,22 +55,54 @@ function chunkifyMaximizeChunkSize(arr, minPerChunk) {
 
 function pkBytes(pk) {
   const b = pk instanceof Uint8Array ? pk : pk.toBytes();
-  if (b.length !== 96) throw Error("pubkey must be 96-byte uncompressed");
+  if (!(b instanceof Uint8Array) || b.length !== 96) throw Error("pubkey must be 96-byte uncompressed");
   return b;
 }
 
-/** jobs: ISignatureSet[][] -> flat typed arrays of the C ABI */
+function setPubkeys(s) {
+  if (s.type === SignatureSetType.single) return [s.pubkey];
+  if (s.type === SignatureSetType.aggregate) return s.pubkeys;
+  throw Error("Unknown signature set type");
+}
+
+/** Checks one call's sets before queueing: a malformed set rejects only its own call. */
+function validateSets(sets) {
+  for (const s of sets) {
+    const pks = setPubkeys(s);
+    if (!Array.isArray(pks)) throw Error("aggregate set needs a pubkeys array");
+    for (const pk of pks) if (!(pk instanceof GpuPublicKey)) pkBytes(pk);
+    const root = s.signingRoot;
+    if (!root || root.length !== 32) throw Error("signing root must be 32 bytes");
+    if (!(s.signature instanceof Uint8Array)) throw Error("signature must be a Uint8Array");
+  }
+}
+
+/** A public key registered in the GPU-resident table (index2pubkey entry). */
+class GpuPublicKey {
+  constructor(index, bytes96) {
+    this.index = index;
+    this.bytes = bytes96;
+  }
+  toBytes() {
+    return this.bytes;
+  }
+}
+
+/** jobs: ISignatureSet[][] -> flat typed arrays of the C ABI (indices when every key has one) */
 function packJobs(jobs) {
   let nSets = 0;
   let nPks = 0;
+  let indexed = true;
   for (const job of jobs)
     for (const s of job) {
       nSets++;
-      nPks += s.type === SignatureSetType.single ? 1 : s.pubkeys.length;
+      const list = setPubkeys(s);
+      nPks += list.length;
+      if (indexed) for (const pk of list) if (!(pk instanceof GpuPublicKey)) indexed = false;
     }
   const jobOff = new Uint32Array(jobs.length + 1);
   const pkOff = new Uint32Array(nSets + 1);
-  const pks = new Uint8Array(nPks * 96);
+  const pks = indexed ? new Uint32Array(nPks) : new Uint8Array(nPks * 96);
   const roots = new Uint8Array(nSets * 32);
   const sigs = new Uint8Array(nSets * 96);
   const sizes = new Uint32Array(nSets);
@@ -70,8 +111,9 @@ function packJobs(jobs) {
   let pi = 0;
   jobs.forEach((job, j) => {
     for (const s of job) {
-      const list = s.type === SignatureSetType.single ? [s.pubkey] : s.pubkeys;
-      for (const pk of list) pks.set(pkBytes(pk), 96 * pi++);
+      const list = setPubkeys(s);
+      if (indexed) for (const pk of list) pks[pi++] = pk.index;
+      else for (const pk of list) pks.set(pkBytes(pk), 96 * pi++);
       pkOff[si + 1] = pi;
       const root = s.signingRoot instanceof Uint8Array ? s.signingRoot : Uint8Array.from(s.signingRoot);
       if (root.length !== 32) throw Error("signing root must be 32 bytes");
@@ -93,16 +135,53 @@ function codeToResult(code) {
 
 class BlsGpuVerifier {
   /**
-   * @param {{device?: number, blsVerifyAllMultiThread?: boolean}} [opts]
+   * @param {{device?: number, engines?: number, blsVerifyAllMultiThread?: boolean}} [opts]
    */
   constructor(opts) {
     opts = opts || {};
-    this.engine = addon.createEngine(opts.device === undefined ? 0 : opts.device);
+    const n = opts.engines === undefined ? 2 : opts.engines;
+    if (!(n >= 1)) throw Error("engines must be >= 1");
+    this.engines = [];
+    for (let k = 0; k < n; k++) this.engines.push(addon.createEngine(opts.device === undefined ? 0 : opts.device));
+    this.idle = this.engines.slice();
     this.blsVerifyAllMultiThread = Boolean(opts.blsVerifyAllMultiThread);
     this.jobs = [];
     this.buffered = null;
-    this.running = null;
+    this.running = new Set();
     this.closed = false;
+    this.stats = {batches: 0, jobs: 0, sets: 0, batchRetries: 0, jobsInvalid: 0, jobsError: 0};
+  }
+
+  /**
+   * Loads keys (each 48-byte compressed or 96-byte uncompressed) into every engine's resident
+   * table once, like the epoch cache's index2pubkey (pubkeyCache.ts:56-77).  Returns handles
+   * usable as ISignatureSet pubkeys.  Keys are decoded on the GPU; a bad key throws its blst error.
+   * @param {Uint8Array[]} keys
+   * @returns {GpuPublicKey[]}
+   */
+  registerPubkeys(keys, validate) {
+    if (keys.length === 0) return [];
+    const size = keys[0].length;
+    if (size !== 48 && size !== 96) throw Error("keys must be 48 or 96 bytes");
+    let flat = new Uint8Array(keys.length * size);
+    keys.forEach((k, i) => {
+      if (k.length !== size) throw Error("keys must all have the same size");
+      flat.set(k, i * size);
+    });
+    if (size === 48) {
+      // decompressed once on the GPU: handles keep the 96-byte form for byte-carrying packages
+      const d = addon.g1Decompress(this.engines[0], flat);
+      for (const st of d.status) if (st !== 0) throw Error(addon.errorName(st));
+      flat = d.out;
+    }
+    let first = -1;
+    for (const e of this.engines) {
+      const r = addon.registerPubkeys(e, flat, 96, Boolean(validate));
+      for (const st of r.status) if (st !== 0) throw Error(addon.errorName(st));
+      if (first >= 0 && r.first !== first) throw Error("engine pubkey tables out of step");
+      first = r.first;
+    }
+    return keys.map((k, i) => new GpuPublicKey(first + i, flat.subarray(96 * i, 96 * i + 96)));
   }
 
   /**
@@ -113,8 +192,9 @@ class BlsGpuVerifier {
   async verifySignatureSets(sets, opts) {
     opts = opts || {};
     if (this.closed) throw new QueueError("QUEUE_ABORTED");
+    validateSets(sets);
     if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
-      const res = addon.verifyJobsSync(this.engine, ...packJobs([sets]));
+      const res = addon.verifyJobsSync(this.engines[0], ...packJobs([sets]));
       return codeToResult(res[0]);
     }
     const results = await Promise.all(
@@ -132,8 +212,10 @@ class BlsGpuVerifier {
       this.buffered = null;
     }
     for (const job of this.jobs.splice(0)) job.reject(new QueueError("QUEUE_ABORTED"));
-    if (this.running) await this.running;
-    addon.destroyEngine(this.engine);
+    await Promise.all([...this.running]);
+    for (const e of this.engines) addon.destroyEngine(e);
+    this.engines = [];
+    this.idle = [];
   }
 
   queueJob(sets, opts) {
@@ -161,30 +243,51 @@ class BlsGpuVerifier {
     setTimeout(() => this.runJobs(), 0);
   }
 
+  /** every idle engine takes the whole queue as one package (multithread/index.ts:290-330) */
   runJobs() {
-    if (this.running || this.jobs.length === 0) return;
-    this.running = (async () => {
-      while (this.jobs.length > 0) {
-        const pkg = this.jobs.splice(0);
-        let codes;
-        try {
-          codes = await addon.verifyJobs(this.engine, ...packJobs(pkg.map((j) => j.sets)));
-        } catch (e) {
-          for (const j of pkg) j.reject(e);
-          continue;
-        }
-        pkg.forEach((j, k) => {
-          if (codes[k] < 0) j.reject(Error(addon.errorName(-codes[k])));
-          else j.resolve(codes[k] === 1);
-        });
+    while (this.idle.length > 0 && this.jobs.length > 0 && !this.closedEngines()) {
+      const engine = this.idle.pop();
+      const pkg = this.jobs.splice(0);
+      const p = this.runPackage(engine, pkg).finally(() => {
+        this.running.delete(p);
+        if (this.engines.includes(engine)) this.idle.push(engine);
+        if (this.jobs.length > 0) this.runJobs();
+      });
+      this.running.add(p);
+    }
+  }
+
+  closedEngines() {
+    return this.engines.length === 0;
+  }
+
+  async runPackage(engine, pkg) {
+    let codes;
+    try {
+      codes = await addon.verifyJobs(engine, ...packJobs(pkg.map((j) => j.sets)));
+    } catch (e) {
+      // device failure: every job of the package rejects (multithread/index.ts:368-375)
+      for (const j of pkg) j.reject(e);
+      return;
+    }
+    this.stats.batches++;
+    this.stats.jobs += pkg.length;
+    pkg.forEach((j, k) => {
+      this.stats.sets += j.sets.length;
+      if (codes[k] < 0) {
+        this.stats.jobsError++;
+        j.reject(Error(addon.errorName(-codes[k])));
+      } else {
+        if (codes[k] === 0) this.stats.jobsInvalid++;
+        j.resolve(codes[k] === 1);
       }
-      this.running = null;
-    })();
+    });
   }
 }
 
 module.exports = {
   BlsGpuVerifier,
+  GpuPublicKey,
   QueueError,
   SignatureSetType,
   chunkifyMaximizeChunkSize,

@@ -12,19 +12,31 @@
  *   - errors come back as codes and become Error objects whose message is the blst error
  *     string ("BLST_INVALID_SIZE", ...), as @chainsafe/blst throws them.
  *
+ *   - request buffers are pinned host memory (lb_host_alloc) from a small free-list pool, so the
+ *     engine's uploads are direct DMA and no page-locking happens per call;
+ *   - argument lengths are checked against the offsets before anything is queued (TypeError).
+ *
  * Exports:
  *   createEngine(device: number) -> External
- *   destroyEngine(engine)
- *   verifyJobs(engine, jobOffsets: Uint32Array, setPkOffsets: Uint32Array, pubkeys: Uint8Array,
+ *       (the first call raises GPU_MAX_HW_QUEUES to 16 unless the environment set it, so the
+ *       two HIP streams of each engine get their own hardware queue)
+ *   destroyEngine(engine)   (deferred until the engine's in-flight requests have settled)
+ *   verifyJobs(engine, jobOffsets: Uint32Array, setPkOffsets: Uint32Array,
+ *              pubkeys: Uint8Array (96 B per key) | pkIndices: Uint32Array (resident table),
  *              signingRoots: Uint8Array, signatures: Uint8Array, sigSizes: Uint32Array | null)
  *     -> Promise<Int32Array>   (per job: 1 valid, 0 invalid, -code rejects)
  *   verifyJobsSync(...same...) -> Int32Array   (verifyOnMainThread path; blocks like the reference)
+ *   registerPubkeys(engine, keys: Uint8Array, keySize: 48 | 96, validate: boolean)
+ *     -> {first: number, status: Int32Array}   (lb_pubkey_table_append: the index2pubkey cache)
+ *   tableSize(engine) -> number
+ *   g1Decompress(engine, keys48: Uint8Array) -> {out: Uint8Array, status: Int32Array}
  *   aggregatePubkeys(engine, setPkOffsets: Uint32Array, pubkeys: Uint8Array)
  *     -> {out: Uint8Array, status: Int32Array}
  *   errorName(code: number) -> string
  */
 #include <node_api.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -40,14 +52,61 @@
 
 typedef struct {
   lb_engine* e;
+  int in_flight;       /* queued/running async requests holding e */
+  int destroy_pending; /* destroyEngine called while requests were in flight */
 } engine_box;
 
 static void engine_finalize(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
   engine_box* b = (engine_box*)data;
+  /* the External is only collected once no request holds a reference to it */
   if (b->e) lb_engine_destroy(b->e);
   free(b);
+}
+
+/* ---------------------------------------------------------------- pinned request buffers */
+/* Free lists of pinned buffers by power-of-two size class (4 KiB .. 2 GiB).  Only the JS thread
+ * allocates and frees (request parse / completion), so no lock is needed. */
+#define POOL_CLASSES 20
+#define POOL_KEEP 8
+typedef struct pin_hdr {
+  struct pin_hdr* next;
+  int cls;
+} pin_hdr;
+static pin_hdr* g_pool[POOL_CLASSES];
+static int g_pool_n[POOL_CLASSES];
+
+static void* pin_alloc(size_t bytes) {
+  int cls = 0;
+  size_t cap = 4096;
+  while (cap < bytes + 64 && cls < POOL_CLASSES - 1) {
+    cap <<= 1;
+    cls++;
+  }
+  if (cap < bytes + 64) return NULL;
+  pin_hdr* h = g_pool[cls];
+  if (h) {
+    g_pool[cls] = h->next;
+    g_pool_n[cls]--;
+  } else {
+    h = (pin_hdr*)lb_host_alloc(cap);
+    if (!h) return NULL;
+    h->cls = cls;
+  }
+  return (uint8_t*)h + 64; /* 64-byte aligned payload */
+}
+
+static void pin_free(void* p) {
+  if (!p) return;
+  pin_hdr* h = (pin_hdr*)((uint8_t*)p - 64);
+  if (g_pool_n[h->cls] >= POOL_KEEP) {
+    lb_host_free(h);
+    return;
+  }
+  h->next = g_pool[h->cls];
+  g_pool[h->cls] = h;
+  g_pool_n[h->cls]++;
 }
 
 static napi_value throw_code(napi_env env, int32_t code) {
@@ -56,11 +115,21 @@ static napi_value throw_code(napi_env env, int32_t code) {
 }
 
 static napi_value create_engine(napi_env env, napi_callback_info info) {
+  static int queues_set = 0;
   size_t argc = 1;
   napi_value argv[1];
   int32_t device = 0;
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   if (argc >= 1) NAPI_CALL(env, napi_get_value_int32(env, argv[0], &device));
+  if (!queues_set) {
+    /* HIP reads GPU_MAX_HW_QUEUES once, at runtime initialisation (the first engine): each
+     * engine drives two streams, and with the default 4 queues the streams of concurrent
+     * engines would share hardware queues (false dependencies).  A value set by the operator
+     * wins; the cap of 32 is the pool's limit. */
+    const char* v = getenv("GPU_MAX_HW_QUEUES");
+    if (!v || !*v) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    queues_set = 1;
+  }
   engine_box* b = (engine_box*)calloc(1, sizeof(engine_box));
   int32_t st = lb_engine_create(device, &b->e);
   if (st != LB_OK) {
@@ -79,93 +148,153 @@ static napi_value destroy_engine(napi_env env, napi_callback_info info) {
   engine_box* b = NULL;
   NAPI_CALL(env, napi_get_value_external(env, argv[0], (void**)&b));
   if (b && b->e) {
-    lb_engine_destroy(b->e);
-    b->e = NULL;
+    if (b->in_flight > 0) {
+      b->destroy_pending = 1; /* the last completing request destroys it */
+    } else {
+      lb_engine_destroy(b->e);
+      b->e = NULL;
+    }
   }
   return NULL;
 }
 
-/* copy a typed array's bytes (null/undefined -> NULL) */
-static int copy_typed(napi_env env, napi_value v, void** out, size_t* nbytes, size_t elem) {
+/* A typed array view: kind, element count and data pointer (null/undefined -> n = 0, data NULL). */
+typedef struct {
+  int present;
+  napi_typedarray_type type;
+  size_t n;
+  void* data;
+} tview;
+
+static int get_view(napi_env env, napi_value v, tview* out) {
   napi_valuetype t;
-  *out = NULL;
-  *nbytes = 0;
+  memset(out, 0, sizeof(*out));
   if (napi_typeof(env, v, &t) != napi_ok) return 0;
   if (t == napi_null || t == napi_undefined) return 1;
   bool is_ta = false;
-  napi_is_typedarray(env, v, &is_ta);
-  if (!is_ta) return 0;
-  napi_typedarray_type tt;
-  size_t len, off;
-  void* data;
+  if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return 0;
   napi_value ab;
-  if (napi_get_typedarray_info(env, v, &tt, &len, &data, &ab, &off) != napi_ok) return 0;
-  size_t bytes = len * elem;
-  *out = malloc(bytes ? bytes : 1);
-  if (bytes) memcpy(*out, data, bytes);
-  *nbytes = bytes;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &out->type, &out->n, &out->data, &ab, &off) != napi_ok) return 0;
+  out->present = 1;
   return 1;
+}
+
+/* pinned copy of the first `bytes` bytes of a view */
+static void* pin_copy(const tview* v, size_t bytes) {
+  void* p = pin_alloc(bytes ? bytes : 1);
+  if (p && bytes) memcpy(p, v->data, bytes);
+  return p;
 }
 
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
   napi_ref engine_ref;
+  engine_box* box;
   lb_engine* e;
   uint32_t n_jobs;
-  uint32_t *job_off, *pk_off, *sig_sizes;
+  int indexed;
+  uint32_t *job_off, *pk_off, *sig_sizes, *pk_idx;
   uint8_t *pks, *roots, *sigs;
   int32_t* out;
   int32_t status;
 } verify_req;
 
 static void free_req(verify_req* r) {
-  free(r->job_off);
-  free(r->pk_off);
-  free(r->sig_sizes);
-  free(r->pks);
-  free(r->roots);
-  free(r->sigs);
+  pin_free(r->job_off);
+  pin_free(r->pk_off);
+  pin_free(r->sig_sizes);
+  pin_free(r->pk_idx);
+  pin_free(r->pks);
+  pin_free(r->roots);
+  pin_free(r->sigs);
   free(r->out);
   free(r);
 }
 
-/* (engine, jobOffsets, setPkOffsets, pubkeys, roots, sigs, sigSizes?) -> request */
+static verify_req* arg_error(napi_env env, verify_req* r, const char* msg) {
+  if (r) free_req(r);
+  napi_throw_type_error(env, NULL, msg);
+  return NULL;
+}
+
+/* (engine, jobOffsets, setPkOffsets, pubkeys | pkIndices, roots, sigs, sigSizes?) -> request.
+ * Every length is checked against what the offsets imply before anything is copied or queued. */
 static verify_req* parse_verify(napi_env env, napi_callback_info info, napi_value* engine_val) {
   size_t argc = 7;
   napi_value argv[7];
-  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 6) {
-    napi_throw_type_error(env, NULL, "verifyJobs(engine, jobOffsets, setPkOffsets, pubkeys, roots, sigs, sigSizes?)");
-    return NULL;
-  }
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 6)
+    return arg_error(env, NULL, "verifyJobs(engine, jobOffsets, setPkOffsets, pubkeys|pkIndices, roots, sigs, sigSizes?)");
   engine_box* b = NULL;
-  if (napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e) {
+  if (napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e || b->destroy_pending) {
     napi_throw_error(env, NULL, "engine destroyed");
     return NULL;
   }
   if (engine_val) *engine_val = argv[0];
+  tview jo, po, pk, rt, sg, sz;
+  memset(&sz, 0, sizeof(sz));
+  if (!get_view(env, argv[1], &jo) || !get_view(env, argv[2], &po) || !get_view(env, argv[3], &pk) ||
+      !get_view(env, argv[4], &rt) || !get_view(env, argv[5], &sg) || (argc >= 7 && !get_view(env, argv[6], &sz)))
+    return arg_error(env, NULL, "expected typed array arguments");
+  if (!jo.present || jo.type != napi_uint32_array || jo.n < 1)
+    return arg_error(env, NULL, "jobOffsets must be a non-empty Uint32Array");
+  if (!po.present || po.type != napi_uint32_array || po.n < 1)
+    return arg_error(env, NULL, "setPkOffsets must be a non-empty Uint32Array");
+  const uint32_t* jof = (const uint32_t*)jo.data;
+  const uint32_t* pof = (const uint32_t*)po.data;
+  const uint32_t n_jobs = (uint32_t)(jo.n - 1);
+  if (jof[0] != 0) return arg_error(env, NULL, "jobOffsets[0] must be 0");
+  for (uint32_t j = 0; j < n_jobs; j++)
+    if (jof[j + 1] < jof[j]) return arg_error(env, NULL, "jobOffsets must be non-decreasing");
+  const uint32_t n_sets = jof[n_jobs];
+  if (po.n != (size_t)n_sets + 1) return arg_error(env, NULL, "setPkOffsets must have jobOffsets[nJobs] + 1 entries");
+  if (pof[0] != 0) return arg_error(env, NULL, "setPkOffsets[0] must be 0");
+  for (uint32_t i = 0; i < n_sets; i++)
+    if (pof[i + 1] < pof[i]) return arg_error(env, NULL, "setPkOffsets must be non-decreasing");
+  const size_t n_pks = pof[n_sets];
+  const int indexed = pk.present && pk.type == napi_uint32_array;
+  if (pk.present && !indexed && pk.type != napi_uint8_array)
+    return arg_error(env, NULL, "pubkeys must be a Uint8Array (96 B per key) or a Uint32Array of table indices");
+  if (indexed ? pk.n < n_pks : (n_pks && (!pk.present || pk.n < n_pks * 96)))
+    return arg_error(env, NULL, "pubkeys shorter than setPkOffsets[nSets] keys");
+  if (!rt.present || rt.type != napi_uint8_array || rt.n < (size_t)n_sets * 32)
+    return arg_error(env, NULL, "signingRoots must be a Uint8Array of 32 B per set");
+  if (!sg.present || sg.type != napi_uint8_array || sg.n < (size_t)n_sets * 96)
+    return arg_error(env, NULL, "signatures must be a Uint8Array of 96 B per set");
+  if (sz.present && (sz.type != napi_uint32_array || sz.n < n_sets))
+    return arg_error(env, NULL, "sigSizes must be a Uint32Array with one entry per set");
   verify_req* r = (verify_req*)calloc(1, sizeof(verify_req));
+  r->box = b;
   r->e = b->e;
-  size_t nb;
-  int ok = copy_typed(env, argv[1], (void**)&r->job_off, &nb, 4);
-  r->n_jobs = nb >= 4 ? (uint32_t)(nb / 4 - 1) : 0;
-  ok &= copy_typed(env, argv[2], (void**)&r->pk_off, &nb, 4);
-  ok &= copy_typed(env, argv[3], (void**)&r->pks, &nb, 1);
-  ok &= copy_typed(env, argv[4], (void**)&r->roots, &nb, 1);
-  ok &= copy_typed(env, argv[5], (void**)&r->sigs, &nb, 1);
-  if (argc >= 7) ok &= copy_typed(env, argv[6], (void**)&r->sig_sizes, &nb, 4);
-  if (!ok || !r->job_off || !r->pk_off) {
+  r->n_jobs = n_jobs;
+  r->indexed = indexed;
+  r->job_off = (uint32_t*)pin_copy(&jo, (size_t)(n_jobs + 1) * 4);
+  r->pk_off = (uint32_t*)pin_copy(&po, (size_t)(n_sets + 1) * 4);
+  if (indexed)
+    r->pk_idx = (uint32_t*)pin_copy(&pk, n_pks * 4);
+  else
+    r->pks = (uint8_t*)pin_copy(&pk, n_pks * 96);
+  r->roots = (uint8_t*)pin_copy(&rt, (size_t)n_sets * 32);
+  r->sigs = (uint8_t*)pin_copy(&sg, (size_t)n_sets * 96);
+  if (sz.present) r->sig_sizes = (uint32_t*)pin_copy(&sz, (size_t)n_sets * 4);
+  r->out = (int32_t*)calloc(n_jobs ? n_jobs : 1, sizeof(int32_t));
+  if (!r->job_off || !r->pk_off || !r->roots || !r->sigs || !r->out || (indexed ? !r->pk_idx : !r->pks) ||
+      (sz.present && !r->sig_sizes)) {
     free_req(r);
-    napi_throw_type_error(env, NULL, "expected Uint32Array / Uint8Array arguments");
+    napi_throw_error(env, NULL, "out of pinned host memory");
     return NULL;
   }
-  r->out = (int32_t*)calloc(r->n_jobs ? r->n_jobs : 1, sizeof(int32_t));
   return r;
 }
 
 static void run_verify(verify_req* r) {
-  r->status = lb_verify_jobs(r->e, r->n_jobs, r->job_off, r->pk_off, r->pks, r->roots, r->sigs, r->sig_sizes,
-                             NULL, r->out);
+  if (r->indexed)
+    r->status = lb_verify_jobs_indexed(r->e, r->n_jobs, r->job_off, r->pk_off, r->pk_idx, r->roots, r->sigs,
+                                       r->sig_sizes, NULL, r->out);
+  else
+    r->status = lb_verify_jobs(r->e, r->n_jobs, r->job_off, r->pk_off, r->pks, r->roots, r->sigs, r->sig_sizes,
+                               NULL, r->out);
 }
 
 static napi_value result_array(napi_env env, verify_req* r) {
@@ -194,6 +323,11 @@ static void complete_verify(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, r->deferred, result_array(env, r));
   }
   napi_delete_async_work(env, r->work);
+  engine_box* b = r->box;
+  if (--b->in_flight == 0 && b->destroy_pending && b->e) {
+    lb_engine_destroy(b->e);
+    b->e = NULL;
+  }
   if (r->engine_ref) napi_delete_reference(env, r->engine_ref);
   free_req(r);
 }
@@ -208,6 +342,7 @@ static napi_value verify_jobs(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_create_string_utf8(env, "lodestar_bls.verifyJobs", NAPI_AUTO_LENGTH, &name));
   NAPI_CALL(env, napi_create_async_work(env, NULL, name, exec_verify, complete_verify, r, &r->work));
   NAPI_CALL(env, napi_queue_async_work(env, r->work));
+  r->box->in_flight++;
   return promise;
 }
 
@@ -229,26 +364,37 @@ static napi_value aggregate_pubkeys(napi_env env, napi_callback_info info) {
   napi_value argv[3];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   engine_box* b = NULL;
-  NAPI_CALL(env, napi_get_value_external(env, argv[0], (void**)&b));
-  if (!b || !b->e) return throw_code(env, LB_ERR_ARGUMENT);
-  uint32_t* off = NULL;
-  uint8_t* pks = NULL;
-  size_t nb_off, nb_pk;
-  if (argc < 3 || !copy_typed(env, argv[1], (void**)&off, &nb_off, 4) ||
-      !copy_typed(env, argv[2], (void**)&pks, &nb_pk, 1) || nb_off < 4) {
-    free(off);
-    free(pks);
+  if (argc < 3 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok) {
     napi_throw_type_error(env, NULL, "aggregatePubkeys(engine, setPkOffsets: Uint32Array, pubkeys: Uint8Array)");
     return NULL;
   }
-  uint32_t n = (uint32_t)(nb_off / 4 - 1);
+  if (!b || !b->e) return throw_code(env, LB_ERR_ARGUMENT);
+  tview off, pk;
+  if (!get_view(env, argv[1], &off) || !get_view(env, argv[2], &pk) || !off.present ||
+      off.type != napi_uint32_array || off.n < 1 || (pk.present && pk.type != napi_uint8_array)) {
+    napi_throw_type_error(env, NULL, "aggregatePubkeys(engine, setPkOffsets: Uint32Array, pubkeys: Uint8Array)");
+    return NULL;
+  }
+  const uint32_t* o = (const uint32_t*)off.data;
+  const uint32_t n = (uint32_t)(off.n - 1);
+  if (o[0] != 0) {
+    napi_throw_type_error(env, NULL, "setPkOffsets[0] must be 0");
+    return NULL;
+  }
+  for (uint32_t i = 0; i < n; i++)
+    if (o[i + 1] < o[i]) {
+      napi_throw_type_error(env, NULL, "setPkOffsets must be non-decreasing");
+      return NULL;
+    }
+  if ((size_t)o[n] * 96 > (pk.present ? pk.n : 0)) {
+    napi_throw_type_error(env, NULL, "pubkeys shorter than setPkOffsets[nSets] keys");
+    return NULL;
+  }
   napi_value ab_o, ab_s, out_o, out_s, obj;
   void *po, *ps;
   NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 96, &po, &ab_o));
   NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &ps, &ab_s));
-  int32_t st = lb_aggregate_pubkeys(b->e, n, off, pks, (uint8_t*)po, (int32_t*)ps);
-  free(off);
-  free(pks);
+  int32_t st = lb_aggregate_pubkeys(b->e, n, o, (const uint8_t*)pk.data, (uint8_t*)po, (int32_t*)ps);
   if (st != LB_OK) return throw_code(env, st);
   NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, (size_t)n * 96, ab_o, 0, &out_o));
   NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab_s, 0, &out_s));
@@ -256,6 +402,78 @@ static napi_value aggregate_pubkeys(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_set_named_property(env, obj, "out", out_o));
   NAPI_CALL(env, napi_set_named_property(env, obj, "status", out_s));
   return obj;
+}
+
+static napi_value register_pubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  if (argc < 3 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e) {
+    napi_throw_type_error(env, NULL, "registerPubkeys(engine, keys: Uint8Array, keySize: 48 | 96, validate?)");
+    return NULL;
+  }
+  tview k;
+  uint32_t key_size = 0;
+  bool validate = false;
+  if (!get_view(env, argv[1], &k) || !k.present || k.type != napi_uint8_array ||
+      napi_get_value_uint32(env, argv[2], &key_size) != napi_ok || (key_size != 48 && key_size != 96) ||
+      k.n % key_size) {
+    napi_throw_type_error(env, NULL, "keys must be a Uint8Array of 48- or 96-byte keys");
+    return NULL;
+  }
+  if (argc >= 4) napi_get_value_bool(env, argv[3], &validate);
+  const uint32_t n = (uint32_t)(k.n / key_size);
+  napi_value ab_s, out_s, obj, first_v;
+  void* ps;
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)(n ? n : 1) * 4, &ps, &ab_s));
+  uint32_t first = 0;
+  int32_t st = lb_pubkey_table_append(b->e, n, (const uint8_t*)k.data, key_size, validate ? 1 : 0, (int32_t*)ps,
+                                      &first);
+  if (st != LB_OK) return throw_code(env, st);
+  NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab_s, 0, &out_s));
+  NAPI_CALL(env, napi_create_uint32(env, first, &first_v));
+  NAPI_CALL(env, napi_create_object(env, &obj));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "first", first_v));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "status", out_s));
+  return obj;
+}
+
+/* g1Decompress(engine, keys48: Uint8Array) -> {out: Uint8Array (96 B per key), status: Int32Array} */
+static napi_value g1_decompress(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview k;
+  if (argc < 2 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &k) || !k.present || k.type != napi_uint8_array || k.n % 48) {
+    napi_throw_type_error(env, NULL, "g1Decompress(engine, keys48: Uint8Array of 48-byte keys)");
+    return NULL;
+  }
+  const uint32_t n = (uint32_t)(k.n / 48);
+  napi_value ab_o, ab_s, out_o, out_s, obj;
+  void *po, *ps;
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 96, &po, &ab_o));
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)n * 4, &ps, &ab_s));
+  int32_t st = lb_g1_decompress(b->e, n, (const uint8_t*)k.data, (uint8_t*)po, (int32_t*)ps, 0);
+  if (st != LB_OK) return throw_code(env, st);
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, (size_t)n * 96, ab_o, 0, &out_o));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, n, ab_s, 0, &out_s));
+  NAPI_CALL(env, napi_create_object(env, &obj));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "out", out_o));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "status", out_s));
+  return obj;
+}
+
+static napi_value table_size(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], v;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  NAPI_CALL(env, napi_get_value_external(env, argv[0], (void**)&b));
+  NAPI_CALL(env, napi_create_uint32(env, b && b->e ? lb_pubkey_table_size(b->e) : 0, &v));
+  return v;
 }
 
 static napi_value error_name(napi_env env, napi_callback_info info) {
@@ -275,6 +493,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"verifyJobs", NULL, verify_jobs, NULL, NULL, NULL, napi_default, NULL},
       {"verifyJobsSync", NULL, verify_jobs_sync, NULL, NULL, NULL, napi_default, NULL},
       {"aggregatePubkeys", NULL, aggregate_pubkeys, NULL, NULL, NULL, napi_default, NULL},
+      {"registerPubkeys", NULL, register_pubkeys, NULL, NULL, NULL, napi_default, NULL},
+      {"tableSize", NULL, table_size, NULL, NULL, NULL, napi_default, NULL},
+      {"g1Decompress", NULL, g1_decompress, NULL, NULL, NULL, napi_default, NULL},
       {"errorName", NULL, error_name, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);

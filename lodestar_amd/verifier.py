@@ -11,10 +11,12 @@ Reference interface and policy (paths under the reference repo):
   * per-job results (worker.ts:32-108): job j resolves true/false or rejects with its error,
     independently of every other job in the same batch (multithread.test.ts:86-103).
 
-The worker threads are replaced by one GPU runner thread per engine: it drains every queued
-job into ONE device batch (one final exponentiation for all valid jobs, bisection over a
-job product tree when it fails), instead of the reference's packages of ~128 sets per CPU
-worker and per-job re-verification.
+The worker threads are replaced by one GPU runner thread per engine (`n_engines` batches in
+flight on the device, default 2): an idle runner drains every queued job into ONE device batch
+(one final exponentiation for all valid jobs, a search for the failing sets when it fails),
+instead of the reference's packages of ~128 sets per CPU worker and per-job re-verification.
+Malformed inputs (root not 32 bytes, pubkey not a PublicKey, signature not bytes) raise in the
+caller's own call before anything is queued, so they never touch other callers' jobs.
 """
 from __future__ import annotations
 
@@ -113,13 +115,17 @@ def _pk_list(s: ISignatureSet) -> List[PublicKey]:
 
 
 def _to_input(s: ISignatureSet) -> SetInput:
-    if s.type == SignatureSetType.single:
-        pks = [s.pubkey.raw]
-    elif s.type == SignatureSetType.aggregate:
-        pks = [p.raw for p in s.pubkeys]
-    else:
-        raise ValueError("Unknown signature set type")
-    return SetInput(pubkeys=pks, signing_root=bytes(s.signing_root), signature=bytes(s.signature))
+    """Validates one set on the caller's side (ValueError) and reduces it to the C ABI's input."""
+    pks = _pk_list(s)
+    for p in pks:
+        if not isinstance(p, PublicKey):
+            raise ValueError("pubkeys must be PublicKey objects")
+    if not isinstance(s.signature, (bytes, bytearray, memoryview)):
+        raise ValueError("signature must be bytes")
+    root = bytes(s.signing_root)
+    if len(root) != 32:
+        raise ValueError("signing root must be 32 bytes")
+    return SetInput(pubkeys=[p.raw for p in pks], signing_root=root, signature=bytes(s.signature))
 
 
 def _result(code: int) -> bool:
@@ -148,11 +154,19 @@ class PoolStats:
 
 
 class BlsGpuVerifier:
-    """IBlsVerifier backed by one MI355X engine (drop-in for BlsMultiThreadWorkerPool)."""
+    """IBlsVerifier backed by MI355X engines (drop-in for BlsMultiThreadWorkerPool)."""
 
-    def __init__(self, engine: Optional[Engine] = None, device: int = 0, bls_verify_all_multi_thread: bool = False):
-        self.engine = engine if engine is not None else Engine(device)
-        self._own_engine = engine is None
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, bls_verify_all_multi_thread: bool = False,
+                 n_engines: int = 2):
+        if engine is not None:
+            self.engines = [engine]
+            self._own_engines = False
+        else:
+            if n_engines < 1:
+                raise ValueError("n_engines must be >= 1")
+            self.engines = [Engine(device) for _ in range(n_engines)]
+            self._own_engines = True
+        self.engine = self.engines[0]
         self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
         self.stats = PoolStats()
         self._lock = threading.Condition()
@@ -161,8 +175,10 @@ class BlsGpuVerifier:
         self._buffered_sigs = 0
         self._buffer_timer: Optional[asyncio.TimerHandle] = None
         self._closed = False
-        self._runner = threading.Thread(target=self._run, name="lodestar-bls-gpu", daemon=True)
-        self._runner.start()
+        self._runners = [threading.Thread(target=self._run, args=(e,), name=f"lodestar-bls-gpu-{k}", daemon=True)
+                         for k, e in enumerate(self.engines)]
+        for t in self._runners:
+            t.start()
 
     # ---------------------------------------------------------------- IBlsVerifier
     async def verify_signature_sets(self, sets: Sequence[ISignatureSet],
@@ -201,19 +217,33 @@ class BlsGpuVerifier:
             self._lock.notify_all()
         for j in pending:
             j.loop.call_soon_threadsafe(_set_exc, j.future, QueueError("QUEUE_ABORTED"))
-        await asyncio.get_running_loop().run_in_executor(None, self._runner.join)
-        if self._own_engine:
-            self.engine.close()
+        for t in self._runners:
+            await asyncio.get_running_loop().run_in_executor(None, t.join)
+        if self._own_engines:
+            for e in self.engines:
+                e.close()
 
     def register_pubkeys(self, pks: Sequence[bytes], validate: bool = False) -> List[PublicKey]:
         """Load keys (48-byte compressed or 96-byte uncompressed) into the GPU-resident table once,
         like the epoch cache's index2pubkey (pubkeyCache.ts:56-77); returned PublicKeys carry their
         table index, so sets built from them ship 4-byte indices instead of 96-byte keys."""
-        first, st = self.engine.pubkey_table_append(list(pks), validate)
-        for s in st:
-            if s:
-                raise BlsError(s)
-        raws = list(pks) if len(pks) and len(pks[0]) == 96 else self.engine.g1_decompress(list(pks))[0]
+        pks = list(pks)
+        if pks and len(pks[0]) == 48:
+            raws, st = self.engine.g1_decompress(pks)
+            for s in st:
+                if s:
+                    raise BlsError(s)
+        else:
+            raws = pks
+        first = None
+        for e in self.engines:  # every engine holds the same table (same indices)
+            f, st = e.pubkey_table_append(raws, validate)
+            for s in st:
+                if s:
+                    raise BlsError(s)
+            if first is not None and f != first:
+                raise RuntimeError("engine pubkey tables out of step")
+            first = f
         return [PublicKey(r, first + k) for k, r in enumerate(raws)]
 
     # ---------------------------------------------------------------- queueing policy
@@ -240,7 +270,7 @@ class BlsGpuVerifier:
             self._lock.notify_all()
 
     # ---------------------------------------------------------------- GPU runner
-    def _run(self):
+    def _run(self, engine: Engine):
         while True:
             with self._lock:
                 while not self._jobs and not self._closed:
@@ -250,15 +280,16 @@ class BlsGpuVerifier:
                 jobs, self._jobs = self._jobs, []
             try:
                 if all(j.idx is not None for j in jobs):
-                    codes = self.engine.verify_jobs_indexed([j.sets for j in jobs], [j.idx for j in jobs])
+                    codes = engine.verify_jobs_indexed([j.sets for j in jobs], [j.idx for j in jobs])
                 else:
-                    codes = self.engine.verify_jobs([j.sets for j in jobs])
+                    codes = engine.verify_jobs([j.sets for j in jobs])
                 err = None
             except Exception as e:  # device failure: every job of the package rejects (index.ts:368-375)
                 codes, err = None, e
-            self.stats.batches += 1
-            self.stats.jobs += len(jobs)
-            self.stats.sets += sum(len(j.sets) for j in jobs)
+            with self._lock:
+                self.stats.batches += 1
+                self.stats.jobs += len(jobs)
+                self.stats.sets += sum(len(j.sets) for j in jobs)
             for k, j in enumerate(jobs):
                 if err is not None:
                     j.loop.call_soon_threadsafe(_set_exc, j.future, err)

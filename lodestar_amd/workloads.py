@@ -21,7 +21,9 @@ Shapes (jobs = verifySignatureSets calls after chunkifyMaximizeChunkSize(sets, 1
       c3_distinct: the same shape with all 19456 roots distinct (the no-sharing bound).
   c4  sync committee: 512 single sync-committee messages + 64 contribution calls (2 singles +
       k=128) + block sync aggregate (k=512) + 4 light-client update aggregates (k=512), with
-      one invalid set per 1000 (configs[3])
+      invalid sets at >= 1/1000 split between well-formed wrong-message signatures (-> false)
+      and malformed bytes (32-byte signature -> BLST_INVALID_SIZE, cleared compression flag
+      -> BLST_BAD_ENCODING), SURVEY.md §8(d) (configs[3])
   c5  range sync: 32 blocks of c2 shape, one call per block (configs[4])
 """
 from __future__ import annotations
@@ -50,6 +52,7 @@ class SetSpec:
     kind: int               # domain-ish tag for the signing root
     invalid: bool = False   # sign a different message (well-formed, wrong)
     root: Optional[int] = None  # sets with equal (kind, root) sign the same message; None = own root
+    malformed: Optional[str] = None  # "short32": 32-byte signature; "flag": compression flag cleared
 
 
 @dataclass
@@ -57,7 +60,7 @@ class Workload:
     name: str
     packed: PackedJobs      # carries both 96-byte keys and pk_indices into the key pool
     n_invalid_jobs: int
-    expected: np.ndarray    # per job 1 / 0
+    expected: np.ndarray    # per job 1 / 0 / -code (the C ABI's out_job convention)
     pool96: Optional[np.ndarray] = None  # the key pool (row k = key of index k)
 
 
@@ -93,17 +96,42 @@ def build(engine: Engine, jobs: Sequence[Sequence[SetSpec]], name: str, keys: Op
     step = 8192
     for a in range(0, n, step):
         sigs[a:a + step] = engine.sign(sks[a:a + step], sign_msgs[a:a + step])
+    sizes = None
+    for i, s in enumerate(flat):
+        if s.malformed == "flag":
+            sigs[i, 0] &= 0x7F                      # compression flag cleared -> BLST_BAD_ENCODING
+        elif s.malformed == "short32":
+            if sizes is None:
+                sizes = np.full(n, 96, dtype=np.uint32)
+            sizes[i] = 32                           # 32-byte signature -> BLST_INVALID_SIZE
+            sigs[i] = 0
     job_off = np.zeros(len(jobs) + 1, dtype=np.uint32)
     job_off[1:] = np.cumsum([len(j) for j in jobs])
     pk_off = np.zeros(n + 1, dtype=np.uint32)
     pk_off[1:] = np.cumsum([len(s.validators) for s in flat])
     vidx = np.fromiter((v % len(keys.sks) for s in flat for v in s.validators), dtype=np.int64)
     pubkeys = np.ascontiguousarray(keys.pk96[vidx].reshape(-1))
-    expected = np.array([0 if any(s.invalid for s in j) else 1 for j in jobs], dtype=np.int32)
+    expected = np.array([expected_code(j) for j in jobs], dtype=np.int32)
     packed = PackedJobs(job_off=job_off, pk_off=pk_off, pubkeys=pubkeys, msgs=msgs.reshape(-1).copy(),
-                        sigs=sigs.reshape(-1).copy(), sig_sizes=None, pk_indices=vidx.astype(np.uint32))
-    return Workload(name=name, packed=packed, n_invalid_jobs=int((expected == 0).sum()), expected=expected,
+                        sigs=sigs.reshape(-1).copy(), sig_sizes=sizes, pk_indices=vidx.astype(np.uint32))
+    return Workload(name=name, packed=packed, n_invalid_jobs=int((expected != 1).sum()), expected=expected,
                     pool96=keys.pk96)
+
+
+LB_BAD_ENCODING = 1
+LB_INVALID_SIZE = 10
+
+
+def expected_code(job: Sequence[SetSpec]) -> int:
+    """Reference verdict of one job of valid keys: the first malformed signature in set order
+    rejects the job (maybeBatch.ts:18-25 decodes every signature before verifying); otherwise any
+    wrong-message set makes it false."""
+    for s in job:
+        if s.malformed == "short32":
+            return -LB_INVALID_SIZE
+        if s.malformed == "flag":
+            return -LB_BAD_ENCODING
+    return 0 if any(s.invalid for s in job) else 1
 
 
 def _block(rng, base_v: int, sync_k: int = 358, att_k: int = 256, n_att: int = 128) -> List[SetSpec]:
@@ -156,6 +184,22 @@ def c3_distinct_specs(rng, **kw):
     return c3_specs(rng, shared=False, **kw)
 
 
+def c3_invalid_specs(rng, slots: int = 1, **kw):
+    """c3 with one planted wrong-message attestation per slot (value_one_invalid_per_batch)."""
+    jobs = c3_specs(rng, slots=slots, **kw)
+    per = len(jobs) // slots
+    for s in range(slots):
+        jobs[s * per + int(rng.integers(0, 16384))][0].invalid = True
+    return jobs
+
+
+def c3_mixed_specs(rng, **kw):
+    """one slot of c3 with the §8(d) invalid mix planted (wrong-message + malformed bytes)."""
+    jobs = c3_specs(rng, **kw)
+    plant_invalid(rng, jobs, 1e-3, min_each=4)
+    return jobs
+
+
 def c4_specs(rng, invalid_rate: float = 1e-3):
     # sync-committee messages and contributions sign this slot's block root; selection proofs
     # sign (slot, subcommittee); the block's sync aggregate signs the previous block root
@@ -167,20 +211,31 @@ def c4_specs(rng, invalid_rate: float = 1e-3):
     jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 7, root=1)])
     for _ in range(4):
         jobs.append([SetSpec([int(x) for x in rng.integers(0, 512, 512)], 10)])
-    n_sets = sum(len(j) for j in jobs)
-    n_bad = max(1, int(round(n_sets * invalid_rate)))
-    flat = [s for j in jobs for s in j]
-    for i in rng.choice(len(flat), n_bad, replace=False):
-        flat[int(i)].invalid = True
+    plant_invalid(rng, jobs, invalid_rate)
     return jobs
+
+
+def plant_invalid(rng, jobs, rate: float, min_each: int = 1):
+    """SURVEY.md §8(d) invalid mix: ceil(rate * sets) bad sets, at least `min_each` of each kind,
+    split between well-formed wrong-message signatures and malformed bytes (32-byte signature,
+    cleared compression flag)."""
+    flat = [s for j in jobs for s in j]
+    n_bad = max(3 * min_each, int(np.ceil(len(flat) * rate)))
+    picks = rng.choice(len(flat), n_bad, replace=False)
+    for k, i in enumerate(picks):
+        kind = k % 3
+        if kind == 0:
+            flat[int(i)].invalid = True
+        else:
+            flat[int(i)].malformed = "short32" if kind == 1 else "flag"
 
 
 def c5_specs(rng, n_blocks: int = 32):
     return [_block(rng, 11 + b) for b in range(n_blocks)]
 
 
-SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c3_distinct": c3_distinct_specs, "c4": c4_specs,
-         "c5": c5_specs}
+SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c3_distinct": c3_distinct_specs,
+         "c3_invalid": c3_invalid_specs, "c3_mixed": c3_mixed_specs, "c4": c4_specs, "c5": c5_specs}
 
 
 def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:

@@ -75,6 +75,48 @@ async function gpuTests() {
   for (let i = 0; i < 8; i++) goods.push(pool.verifySignatureSets(k4, {batchable: true}));
   assert.strictEqual(await bad, "BLST_INVALID_SIZE");
   assert.deepStrictEqual(await Promise.all(goods), Array(8).fill(true));
+  // a malformed set rejects only its own call, before anything is queued (ADVICE r1)
+  const shortRoot = {...k4[0], signingRoot: new Uint8Array(31)};
+  const mixed = await Promise.all([
+    outcome(pool.verifySignatureSets([shortRoot], {batchable: true})),
+    outcome(pool.verifySignatureSets(k4, {batchable: true})),
+  ]);
+  assert.deepStrictEqual(mixed, ["signing root must be 32 bytes", true]);
+  // resident pubkey table: registered handles ship 4-byte indices; mixing them with raw keys
+  // falls back to bytes for that package
+  const keys = golden("reference_kats.json").K4_multithread_sets.sets.map((s) => hex(s.pubkey96));
+  const handles = pool.registerPubkeys(keys);
+  assert.strictEqual(handles.length, keys.length);
+  const k4idx = k4.map((s, i) => ({...s, pubkey: handles[i]}));
+  const packedIdx = m.packJobs([k4idx]);
+  assert.ok(packedIdx[2] instanceof Uint32Array);
+  const idxRes = await Promise.all([
+    pool.verifySignatureSets(k4idx, {batchable: true}),
+    pool.verifySignatureSets([k4idx[0], k4[1]], {batchable: true}),
+    pool.verifySignatureSets(k4idx, {verifyOnMainThread: true}),
+    outcome(pool.verifySignatureSets([{...k4idx[0], signingRoot: k4[1].signingRoot}], {batchable: true})),
+  ]);
+  assert.deepStrictEqual(idxRes, [true, true, true, false]);
+  // compressed keys register too (decompressed on the GPU)
+  const k1 = golden("reference_kats.json").K1_interop_pubkeys.pubkeys.slice(0, 4).map(hex);
+  const h1 = pool.registerPubkeys(k1, true);
+  assert.strictEqual(h1[0].toBytes().length, 96);
+  // addon argument checks: lengths must match the offsets (TypeError, nothing queued)
+  const eng = m.addon.createEngine(0);
+  const jo = Uint32Array.from([0, 1]);
+  const po = Uint32Array.from([0, 1]);
+  assert.throws(() => m.addon.verifyJobs(eng, jo, po, new Uint8Array(95), new Uint8Array(32), new Uint8Array(96)), TypeError);
+  assert.throws(() => m.addon.verifyJobs(eng, jo, po, new Uint8Array(96), new Uint8Array(31), new Uint8Array(96)), TypeError);
+  assert.throws(() => m.addon.verifyJobs(eng, jo, po, new Uint8Array(96), new Uint8Array(32), new Uint8Array(95)), TypeError);
+  assert.throws(() => m.addon.verifyJobs(eng, jo, Uint32Array.from([0]), new Uint8Array(96), new Uint8Array(32), new Uint8Array(96)), TypeError);
+  assert.throws(() => m.addon.verifyJobs(eng, Uint32Array.from([0, 2, 1]), po, new Uint8Array(96), new Uint8Array(32), new Uint8Array(96)), TypeError);
+  assert.throws(() => m.addon.verifyJobs(eng, jo, po, new Uint8Array(96), new Uint8Array(32), new Uint8Array(96), new Uint32Array(0)), TypeError);
+  // destroyEngine while a request is in flight: deferred until it settles
+  const single = m.packJobs([[k4[0]]]);
+  const inflight = m.addon.verifyJobs(eng, ...single);
+  m.addon.destroyEngine(eng);
+  assert.deepStrictEqual(Array.from(await inflight), [1]);
+  assert.throws(() => m.addon.verifyJobs(eng, ...single), /engine destroyed/);
   // close(): queued jobs abort
   const pending = outcome(pool.verifySignatureSets(k4, {batchable: true}));
   await pool.close();

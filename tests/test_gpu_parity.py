@@ -417,7 +417,7 @@ def test_baseline_config_workloads(engine, name):
     wl = W.make(engine, name)
     p = wl.packed
     b = engine.upload(W.PackedJobs(job_off=p.job_off, pk_off=p.pk_off, pubkeys=p.pubkeys, msgs=p.msgs,
-                                   sigs=p.sigs, sig_sizes=None))
+                                   sigs=p.sigs, sig_sizes=p.sig_sizes))
     try:
         got = np.asarray(b.verify())[:p.n_jobs]
     finally:
@@ -431,3 +431,66 @@ def test_baseline_config_workloads(engine, name):
     assert np.array_equal(got, wl.expected)
     if name == "c4":
         assert wl.n_invalid_jobs >= 1
+
+
+@pytest.mark.parametrize("name", ["c3", "c3_mixed"])
+def test_c3_one_slot_workload(engine, name):
+    """The headline config's one-slot shape (19 456 sets, 17 408 jobs, roots shared per committee)
+    through the HIP path; c3_mixed plants the §8(d) invalid mix (wrong-message signatures and
+    malformed bytes: 32-byte signatures, cleared compression flags).  Per-job verdicts must equal
+    the planted expectation through both the resident-table and the 96-byte-key paths."""
+    from lodestar_amd import workloads as W
+    wl = W.make(engine, name)
+    p = wl.packed
+    assert p.n_sets == 19456 and p.n_jobs == 17408
+    bi = engine.upload(W.indexed_for(engine, wl))
+    try:
+        got = np.asarray(bi.verify())[:p.n_jobs]
+    finally:
+        bi.free()
+    assert np.array_equal(got, wl.expected), (name, np.nonzero(got != wl.expected))
+    b = engine.upload(W.PackedJobs(job_off=p.job_off, pk_off=p.pk_off, pubkeys=p.pubkeys, msgs=p.msgs,
+                                   sigs=p.sigs, sig_sizes=p.sig_sizes))
+    try:
+        got = np.asarray(b.verify())[:p.n_jobs]
+    finally:
+        b.free()
+    assert np.array_equal(got, wl.expected)
+    if name == "c3_mixed":
+        assert (wl.expected == 0).sum() >= 4
+        assert (wl.expected == -W.LB_INVALID_SIZE).sum() >= 4 and (wl.expected == -W.LB_BAD_ENCODING).sum() >= 4
+
+
+def test_verify_jobs_workspace_reuse_and_indexed(engine):
+    """lb_verify_jobs / lb_verify_jobs_indexed reuse one engine-owned workspace: shrinking and
+    growing calls back to back give the same verdicts as resident batches."""
+    from lodestar_amd import workloads as W
+    wl = W.make(engine, "c1")
+    p = W.PackedJobs(job_off=wl.packed.job_off, pk_off=wl.packed.pk_off, pubkeys=wl.packed.pubkeys,
+                     msgs=wl.packed.msgs, sigs=wl.packed.sigs, sig_sizes=None)   # 96-byte keys
+    ip = W.indexed_for(engine, wl)                                              # table indices
+    for _ in range(2):
+        assert engine.verify_jobs_packed(p) == list(wl.expected)
+        assert engine.verify_jobs_packed(ip) == list(wl.expected)
+        small = make_batch(engine, 3, seed=41, invalid={1})
+        assert engine.verify_jobs(small) == [1, 0, 1]
+
+
+def test_indexed_null_indices_only_without_keys(engine):
+    from lodestar_amd import _native as N
+    import ctypes
+    lib = N.load()
+    job_off = np.array([0, 1], dtype=np.uint32)
+    pk_off = np.array([0, 1], dtype=np.uint32)          # one key but no index array
+    msgs = np.zeros(32, np.uint8)
+    sigs = np.zeros(96, np.uint8)
+    out = np.zeros(1, np.int32)
+    p32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
+    p8 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))  # noqa: E731
+    st = lib.lb_verify_jobs_indexed(engine.h, 1, p32(job_off), p32(pk_off), None, p8(msgs), p8(sigs), None, None,
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    assert st == N.LB_ERR_ARGUMENT
+    pk0 = np.array([0, 0], dtype=np.uint32)             # no keys: valid call, the set rejects
+    st = lib.lb_verify_jobs_indexed(engine.h, 1, p32(job_off), p32(pk0), None, p8(msgs), p8(sigs), None, None,
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    assert st == N.LB_OK and out[0] == -N.LB_EMPTY_AGGREGATE_ARRAY

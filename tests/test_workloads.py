@@ -32,3 +32,34 @@ def test_c4_sync_committee_roots():
     # 64 contribution-and-proof roots, 4 light-client update roots
     assert n_roots == 1 + 4 + 1 + 64 + 4
     assert sum(s.invalid for j in jobs for s in j) >= 1
+
+
+def test_c4_invalid_mix_follows_survey():
+    """>= 1/1000 invalid sets, split between well-formed wrong-message
+    signatures (-> false) and malformed bytes (32-byte signature, cleared flag -> reject)."""
+    jobs = W.c4_specs(np.random.default_rng(W.SEED))
+    flat = [s for j in jobs for s in j]
+    wrong = sum(s.invalid for s in flat)
+    short = sum(s.malformed == "short32" for s in flat)
+    flag = sum(s.malformed == "flag" for s in flat)
+    assert wrong >= 1 and short >= 1 and flag >= 1
+    assert wrong + short + flag >= len(flat) / 1000
+
+
+def test_expected_code_precedence():
+    S = W.SetSpec
+    assert W.expected_code([S([1], 0)]) == 1
+    assert W.expected_code([S([1], 0, invalid=True)]) == 0
+    # a malformed signature rejects the job even when another set is merely wrong
+    assert W.expected_code([S([1], 0, invalid=True), S([2], 0, malformed="flag")]) == -W.LB_BAD_ENCODING
+    assert W.expected_code([S([1], 0, malformed="short32"), S([2], 0, malformed="flag")]) == -W.LB_INVALID_SIZE
+
+
+def test_c3_invalid_and_mixed_shapes():
+    jobs = W.c3_invalid_specs(np.random.default_rng(W.SEED), slots=2)
+    assert len(jobs) == 2 * 17408
+    assert sum(s.invalid for j in jobs for s in j) == 2
+    mixed = W.c3_mixed_specs(np.random.default_rng(W.SEED))
+    flat = [s for j in mixed for s in j]
+    assert sum(s.invalid for s in flat) >= 4
+    assert sum(s.malformed == "short32" for s in flat) >= 4 and sum(s.malformed == "flag" for s in flat) >= 4
