@@ -5,27 +5,39 @@ x 3 sets = 17408 jobs / 19456 sets, signing roots shared per committee as on mai
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3] [--slots B] [--inflight F]
 
-One process per GPU (torchrun for N>1; RANK/LOCAL_RANK/WORLD_SIZE from the env).  Each rank
-verifies its own shard (weak scaling: sets shard across GPUs with no data-path collective; the
-optional --exchange flag adds the 576-byte Fp12 partial all-gather over RCCL and one final
-exponentiation).  A batch = B slots of gossip drained into one device batch
-(default 6); F batches are in flight per GPU (default 4, independent engines): ~66 ms per batch
-under load (profiles/r1_slots_sweep.txt).  A step =
+One process per GPU.  Under torchrun (WORLD_SIZE set) every rank runs main(); `--gpus N` with
+N > 1 and no WORLD_SIZE relaunches itself under torch.distributed.run (127.0.0.1) before any GPU
+call.  Each rank verifies its own shard (weak scaling: sets shard across GPUs with no data-path
+collective; --exchange adds the 576-byte Fp12 partial all-gather over RCCL and one final
+exponentiation per step).  A batch = B slots of gossip drained into one device
+batch (default 6); F batches are in flight per GPU (default 6, independent engines).  A step =
 lb_batch_verify over one resident batch: all kernels + CSPRNG scalars + per-job result readback.
-Inputs are in HBM before the timed region.  Rank 0 prints one JSON line; value_distinct_roots is
-the same measurement with every signing root distinct (the no-sharing bound).
+Inputs are in HBM before the timed region.  Rank 0 prints one JSON line.
+
+Secondary measurements on the same line (rank 0; N = 1 unless noted):
+  value_one_batch_in_flight     one engine, the same batch
+  value_distinct_roots          every signing root distinct (the no-sharing bound)
+  value_one_invalid_per_batch   one wrong-message attestation per slot (the invalid-set search)
+  value_slots1                  one slot per batch, one batch in flight (+ its latency)
+  latency_1set_ms / latency_block_ms   one 1-set call / one c2 block call through lb_verify_jobs
+  per_config                    c1, c2, c4, c5 at one batch in flight (resident, lb_batch_verify)
+  value_dropin                  c3 through the JS IBlsVerifier (tools/bench_dropin.js): JS
+                                marshalling + pinned copy + H2D inside the timed region
+  cpu_baseline / cpu_c1         the reference worker policy on host cores (oracle/cpu_pool.cpp)
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Each engine drives two HIP streams; HIP's default of 4 hardware queues per process would make
-# the 12 streams of 6 batches in flight share queues (false dependencies between independent
+# the streams of the batches in flight share queues (false dependencies between independent
 # batches).  16 queues (HIP reads this at runtime init, before any GPU call below) gives every
 # stream its own.  Measured on MI355X: profiles/r1_inflight_sweep.txt.  The GPU boxes export
 # GPU_MAX_HW_QUEUES=4, so raise it rather than only defaulting it.
@@ -53,7 +65,23 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-distinct", action="store_true",
                     help="skip the secondary measurement with every signing root distinct (c3_distinct)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary legs (invalid-set, slots1, latencies, per-config, drop-in)")
+    ap.add_argument("--dropin-engines", type=int, default=4)
     return ap.parse_args()
+
+
+def relaunch_distributed(a):
+    """`bench.py --gpus N` outside torchrun: start N ranks (one per GPU) under
+    torch.distributed.run before this process touches the GPU, and exit with its code."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def load_counts():
@@ -78,10 +106,6 @@ def stage_work(counts, packed):
     c = counts["fp_mul_per_item"]
     n = packed.n_sets
     nu = n_roots(packed)
-    sets_per_job = np.diff(packed.job_off.astype(np.int64))
-    m = 1
-    while m < packed.n_jobs:
-        m *= 2
     n_keys = int(packed.pk_off[-1])
     return {
         "decode_sigs": n * c["decode_sigs"],
@@ -120,14 +144,14 @@ def roofline(counts, packed, stage_ms):
     if os.path.exists(tp):
         with open(tp) as f:
             t = json.load(f)
-        k = t.get("kernels", {}).get("k_" + dom)
+        k = t.get("stages", {}).get(dom)
         if k and k.get("sets_per_launch") == packed.n_sets:
             traffic = k["bytes_per_launch"]
-    return {"bound": "valu-int", "kernel": "k_" + dom, "achieved": ach, "peak": peak,
+    return {"bound": "valu-int", "kernel": "stage " + dom, "achieved": ach, "peak": peak,
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": traffic,
-            "traffic_note": "HBM bytes per launch from FETCH_SIZE + WRITE_SIZE (profiles/traffic.json, "
-                            "rocprofv3 --pmc at this config); mostly register-spill scratch: the algorithmic "
-                            "bytes are ~300 B per set (DESIGN.md section 5)",
+            "traffic_note": "HBM bytes per launch of the stage's kernels from FETCH_SIZE + WRITE_SIZE "
+                            "(profiles/traffic.json, rocprofv3 --pmc at this config); the algorithmic bytes "
+                            "are ~300 B per set (DESIGN.md section 5)",
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}
 
@@ -154,16 +178,118 @@ def run_inflight(batches, steps, expected, barrier):
     barrier()
     el = time.perf_counter() - t1
     for r in res:
-        assert np.array_equal(np.asarray(r) == 1, expected == 1), "verification results differ"
+        assert np.array_equal(np.asarray(r), expected), "verification results differ"
     return el
+
+
+def median_ms(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return round(float(np.median(ts)), 3)
+
+
+def extra_legs(a, engs, barrier, W):
+    """Secondary measurements (rank 0 at N = 1; each bounded to a few seconds)."""
+    out = {}
+    eng = engs[0]
+    # one invalid attestation per slot: the failing root's search, batches in flight
+    wi = W.make(eng, "c3_invalid", slots=a.slots)
+    batches = [e.upload(W.indexed_for(e, wi)) for e in engs]
+    codes = batches[0].verify()
+    assert np.array_equal(np.asarray(codes), wi.expected), "invalid-set search verdicts differ"
+    steps = max(2, a.steps // 2)
+    if len(engs) > 1:
+        el = run_inflight(batches, steps, wi.expected, barrier)
+    else:
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            batches[0].verify()
+        barrier()
+        el = time.perf_counter() - t1
+    out["value_one_invalid_per_batch"] = round(wi.packed.n_sets * steps * len(engs) / el, 1)
+    eng.set_profiling(True)
+    batches[0].verify()
+    prof = eng.last_profile()
+    eng.set_profiling(False)
+    out["invalid_batch_stage_ms"] = {k: round(v, 3) for k, v in prof.items() if v > 0}
+    for b in batches:
+        b.free()
+    # one slot per batch, one batch in flight
+    w1 = W.make(eng, "c3")
+    b1 = eng.upload(W.indexed_for(eng, w1))
+    b1.verify()
+    lat = median_ms(lambda: b1.verify(), max(3, a.steps))
+    out["value_slots1"] = round(w1.packed.n_sets / (lat * 1e-3), 1)
+    out["latency_slot1_ms"] = lat
+    b1.free()
+    # small calls through the workspace path (lb_verify_jobs_indexed: upload + verify + readback)
+    wc1 = W.make(eng, "c1")
+    ip = W.indexed_for(eng, wc1)
+    one = W.PackedJobs(job_off=np.array([0, 1], np.uint32), pk_off=np.array([0, 1], np.uint32), pubkeys=None,
+                       msgs=ip.msgs[:32], sigs=ip.sigs[:96], sig_sizes=None, pk_indices=ip.pk_indices[:1])
+    assert eng.verify_jobs_packed(one) == [1]
+    out["latency_1set_ms"] = median_ms(lambda: eng.verify_jobs_packed(one), 10)
+    wc2 = W.make(eng, "c2")
+    ip2 = W.indexed_for(eng, wc2)
+    assert eng.verify_jobs_packed(ip2) == list(wc2.expected)
+    out["latency_block_ms"] = median_ms(lambda: eng.verify_jobs_packed(ip2), 10)
+    # the other BASELINE configs at one batch in flight (resident inputs)
+    per = {}
+    for name in ("c1", "c2", "c4", "c5"):
+        wl = W.make(eng, name)
+        b = eng.upload(W.indexed_for(eng, wl))
+        got = b.verify()
+        assert np.array_equal(np.asarray(got), wl.expected), name
+        ms = median_ms(lambda: b.verify(), 3)
+        per[name] = {"sets": wl.packed.n_sets, "jobs": wl.packed.n_jobs, "ms_per_batch": ms,
+                     "sets_per_s": round(wl.packed.n_sets / (ms * 1e-3), 1),
+                     "invalid_or_rejected_jobs": int((wl.expected != 1).sum())}
+        b.free()
+    out["per_config"] = per
+    return out, wc1
+
+
+def dropin_leg(a, W, eng_factory):
+    """c3 through the JS IBlsVerifier in a node child process (tools/bench_dropin.js)."""
+    import shutil
+    node = shutil.which("node")
+    if node is None:
+        return {"error": "node not installed"}
+    e = eng_factory()
+    try:
+        wl = W.make(e, "c3", slots=a.slots) if a.slots > 1 else W.make(e, "c3")
+    finally:
+        e.close()
+    p = wl.packed
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        hdr = np.array([0x4C424430, len(wl.pool96), p.n_jobs, p.n_sets, int(p.pk_off[-1]), a.slots], np.uint32)
+        for arr in (hdr, np.ascontiguousarray(wl.pool96, np.uint8), p.job_off.astype(np.uint32),
+                    p.pk_off.astype(np.uint32), p.pk_indices.astype(np.uint32), p.msgs, p.sigs,
+                    wl.expected.astype(np.int32)):
+            f.write(np.ascontiguousarray(arr).tobytes())
+        path = f.name
+    try:
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "bench_dropin.js"), path, str(a.dropin_engines), "3"],
+                           capture_output=True, text=True, timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-500:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def main():
     a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(a))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (not used by the driver): LB_BENCH_BACKEND=gloo + LB_BENCH_DEVICE=0 run N ranks
@@ -172,12 +298,14 @@ def main():
     if os.environ.get("LB_BENCH_DEVICE") is not None:
         local = int(os.environ["LB_BENCH_DEVICE"])
     coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+    world_seen = 1
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world_seen = dist.get_world_size()
 
     from lodestar_amd.engine import Engine
     from lodestar_amd import workloads as W
@@ -216,7 +344,7 @@ def main():
 
     for _ in range(a.warmup):
         codes = step()
-    assert np.array_equal(np.asarray(codes) == 1, wl.expected == 1), "verification results differ from expected"
+    assert np.array_equal(np.asarray(codes), wl.expected), "verification results differ from expected"
 
     # (1) one batch in flight: K profiled steps (per-stage HIP-event times feed the roofline)
     stage_ms = {}
@@ -232,7 +360,8 @@ def main():
     eng.set_profiling(False)
     stage_ms = {k: v / a.steps for k, v in stage_ms.items()}
     el = el_single
-    if a.inflight > 1:
+    inflight = a.inflight if not a.exchange else 1
+    if inflight > 1:
         el = run_inflight(batches, a.steps, wl.expected, barrier)
     el_t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
     if world > 1:
@@ -242,8 +371,8 @@ def main():
     if world > 1:
         dist.all_reduce(es_t, op=dist.ReduceOp.MAX)
     value_single = n_sets * world * a.steps / float(es_t.item())
-    ms_per_step = el / (a.steps * a.inflight) * 1e3
-    value = n_sets * world * a.steps * a.inflight / el
+    ms_per_step = el / (a.steps * inflight) * 1e3
+    value = n_sets * world * a.steps * inflight / el
 
     roof = roofline(load_counts(), wl.packed, stage_ms)
     # secondary: the same slot shape with every signing root distinct (no sharing to exploit)
@@ -266,34 +395,54 @@ def main():
         if world > 1:
             dist.all_reduce(eld_t, op=dist.ReduceOp.MAX)
         value_distinct = wd.packed.n_sets * world * a.steps * a.inflight / float(eld_t.item())
-    cpu = None
+    for b in batches:
+        b.free()
+    solo = rank == 0 and world == 1 and not a.no_extra and a.workload == "c3" and not a.exchange
+    extra, dropin, wc1 = {}, None, None
+    if solo:
+        extra, wc1 = extra_legs(a, engs, barrier, W)
+    for e in engs:
+        e.close()
+    if solo:
+        try:
+            dropin = dropin_leg(a, W, lambda: Engine(local))
+        except Exception as e:  # reported, never fatal
+            dropin = {"error": repr(e)}
+    cpu = cpu_c1 = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            from oracle.cpu_pool import time_cpu_pool
-            cpu = time_cpu_pool(wl.packed, seconds=a.cpu_seconds, threads=a.cpu_threads)
+            from oracle.cpu_pool import time_c1, time_cpu_pool
+            cpu = time_cpu_pool(wl.packed, seconds=a.cpu_seconds, threads=a.cpu_threads,
+                                batchable=a.workload.startswith("c3"))
+            if wc1 is not None:
+                cpu_c1 = time_c1(wc1.packed)
         except Exception as e:  # reported, never fatal
             cpu = {"error": repr(e)}
 
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "verified signature sets/sec (mainnet attestation mix)",
             "value": round(value, 1), "unit": "sets/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)", "data": "synthetic",
+            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery; device products on 14x28-bit limbs)",
+            "data": "synthetic",
             "config": {"workload": (f"{a.workload}: gossip attestation flood, {a.slots} slot(s) per batch, "
-                                    f"{a.inflight} batches in flight per GPU") if a.workload == "c3" else a.workload,
+                                    f"{inflight} batches in flight per GPU") if a.workload == "c3" else a.workload,
                        "slots_per_batch": a.slots, "sets_per_gpu": n_sets, "jobs_per_gpu": n_jobs,
                        "pubkeys_per_gpu": int(wl.packed.pk_off[-1]), "parallelism": f"dp{world} (sets sharded)",
-                       "exchange": bool(a.exchange), "inflight": a.inflight,
+                       "exchange": bool(a.exchange), "inflight": inflight, "world_size_seen": world_seen,
                        "pubkeys": "96-byte keys per set" if a.pubkey_bytes else "indices into the GPU-resident table",
                        "signing_roots_per_gpu": n_roots(wl.packed)},
             "value_one_batch_in_flight": round(value_single, 1),
             "batch_latency_ms": round(el / a.steps * 1e3, 1),
             "value_distinct_roots": None if value_distinct is None else round(value_distinct, 1),
-            "roofline": roof, "cpu_baseline": cpu, "gen_s": round(gen_s, 2),
-        }), flush=True)
-    for e in engs:
-        e.close()
+        }
+        line.update(extra)
+        if dropin is not None:
+            line["value_dropin"] = dropin.get("value_dropin")
+            line["dropin"] = dropin
+        line.update({"roofline": roof, "cpu_baseline": cpu, "cpu_c1": cpu_c1, "gen_s": round(gen_s, 2)})
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -11,6 +11,7 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -61,14 +62,14 @@ enum {
   ST_TREE_P,      // s1
   ST_ML_S,        // s2
   ST_ROOT,        // s1 (after joining s2)
-  ST_FALLBACK,    // s1
-  ST_BISECT,      // s1
+  ST_FALLBACK,    // s1: invalid-set search, range MSMs + part sums
+  ST_BISECT,      // s1: invalid-set search, node checks
   ST_TOTAL,
   kStages
 };
 const char* const kStageNames[kStages] = {"decode_sigs", "dedup",   "hash_map", "hash_finish", "pk_chunks",
                                           "pk_blind",    "sig_msm", "group_sum", "miller",    "tree_up_P",
-                                          "ml_S",        "root_check", "fallback", "bisect",   "total"};
+                                          "ml_S",        "root_check", "search_msm", "search_check", "total"};
 
 }  // namespace
 
@@ -107,6 +108,8 @@ struct lb_engine {
       set_live, gacc, gp_aff, gp_inf;
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum;
+  // invalid-set search (search_invalid): node descriptors and per-node results
+  dbuf srch_kind, srch_key, srch_lo, srch_len, srch_pre, srch_S, srch_pk, srch_verdict;
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -253,7 +256,8 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
-                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum};
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->srch_kind, &e->srch_key,
+                  &e->srch_lo, &e->srch_len, &e->srch_pre, &e->srch_S, &e->srch_pk, &e->srch_verdict};
   for (dbuf* b : bufs) b->release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
@@ -511,9 +515,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->q.ensure((size_t)ns * 2 * sizeof(g2j)));
   LB_HIP(e->h_aff.ensure((size_t)ns * sizeof(g2a)));
   LB_HIP(e->rpk.ensure((size_t)ns * sizeof(g1j)));
-  LB_HIP(e->rsig.ensure((size_t)ns * sizeof(g2j)));
   LB_HIP(e->pk_status.ensure((size_t)ns * 4));
-  LB_HIP(e->ml.ensure((size_t)ns * sizeof(fp12)));
   LB_HIP(e->treeP.ensure((size_t)2 * mt * sizeof(fp12)));
   LB_HIP(e->treeS.ensure((size_t)2 * mj * sizeof(g2j)));
   LB_HIP(e->job_status.ensure((size_t)(nj ? nj : 1) * 4));
@@ -635,11 +637,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
-                         e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>());
+                         e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(LB_MSM_NB)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
-                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>());
-      hipLaunchKernelGGL(k_msm_reduce, dim3(1), dim3(64), 0, s2, e->bsum.as<uint32_t>(), 2 * mj,
-                         e->treeS.as<uint32_t>());
+                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB);
+      hipLaunchKernelGGL(k_msm_reduce, dim3(1), dim3(64), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
+                         e->treeS.as<uint32_t>(), 2 * mj, 1u);
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
     LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
@@ -685,47 +687,184 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   return LB_OK;
 }
 
-// Per-set fallback after a failing root: per-set Miller loops and the job product tree
-// (leaves = jobs, rejecting jobs are identity), the structure the bisection walks.
-static int32_t run_fallback(lb_engine* e, lb_batch* b, uint32_t mj) {
-  const uint32_t n = b->n_sets, nj = b->n_jobs;
+// ---------------------------------------------------------------- invalid-set search
+// After a failing root check: find the failing SETS (a job fails iff one of its live sets does;
+// per-job verdicts then equal the reference's per-job re-verification, worker.ts:76-98, up to
+// the 2^-64 soundness of the blinding).  Nodes are ranges of the members array (sets sorted by
+// signing root, lb_kernels.h k_search_check): first subtrees of the root product tree (P from
+// the tree, no new Miller loop), then parts of one failing root (P = one Miller loop of the
+// part's sum r_i PK_i with that root's H(m)), each checked with one final exponentiation, with a
+// fan-out of up to 256 (first level) / 64 nodes, so a single invalid set among ~10^5 is found in
+// about four levels of wave-parallel checks.  Costs scale with the failing ranges, not the batch:
+// the range MSMs touch each member once per level it is under a failing node.
+namespace {
+struct search_node {
+  uint32_t kind, key, lo, len;  // kind 0: key = heap index in the root tree; 1: key = root id
+  int32_t parent;               // index of the failing node this one refines (-1: the root)
+};
+}  // namespace
+
+static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& nd, size_t a, size_t c, uint32_t n,
+                                  uint32_t mu, std::vector<int32_t>& verdict) {
   hipStream_t s1 = e->stream;
-  stage_scope sc(e, ST_FALLBACK, s1);
-  if (n)
-    hipLaunchKernelGGL(k_miller, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rpk.as<uint32_t>(),
-                       e->h_aff.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->pk_status.as<int32_t>(),
-                       e->ml.as<uint32_t>());
-  hipLaunchKernelGGL(k_job_leaves_P, dim3(nblk(mj)), dim3(LB_TPB), 0, s1, nj, n, mj, b->d_job_off.as<uint32_t>(),
-                     e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->ml.as<uint32_t>(),
-                     e->treeP.as<uint32_t>(), e->job_status.as<int32_t>());
-  for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
-    hipLaunchKernelGGL(k_tree_up_P, dim3(lo), dim3(64), 0, s1, mj, lo, e->treeP.as<uint32_t>());
-  // per-job signature sums (the MSM only formed the root)
-  if (n)
-    hipLaunchKernelGGL(k_sig_blind, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->scalars.as<uint64_t>(),
-                       e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(),
-                       e->rsig.as<uint32_t>());
-  hipLaunchKernelGGL(k_job_leaves_S, dim3(nblk(mj)), dim3(LB_TPB), 0, s1, nj, n, mj, b->d_job_off.as<uint32_t>(),
-                     e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->rsig.as<uint32_t>(),
-                     e->treeS.as<uint32_t>());
-  for (uint32_t lo = mj / 2; lo >= 1; lo /= 2)
-    hipLaunchKernelGGL(k_tree_up_S, dim3(nblk(lo)), dim3(LB_TPB), 0, s1, mj, lo, e->treeS.as<uint32_t>());
+  std::vector<uint32_t> hk(c), hkey(c), hlo(c), hlen(c), pre(c + 1);
+  pre[0] = 0;
+  for (size_t j = 0; j < c; j++) {
+    hk[j] = nd[a + j].kind;
+    hkey[j] = nd[a + j].key;
+    hlo[j] = nd[a + j].lo;
+    hlen[j] = nd[a + j].len;
+    pre[j + 1] = pre[j] + hlen[j];
+  }
+  const uint32_t T = pre[c], nb = (uint32_t)c * LB_MSM_NB;
+  const uint32_t bcap = (2 * LB_MSM_W * T) / LB_GROUP_CHUNK + nb;
+  LB_HIP(e->srch_kind.ensure(c * 4));
+  LB_HIP(e->srch_key.ensure(c * 4));
+  LB_HIP(e->srch_lo.ensure(c * 4));
+  LB_HIP(e->srch_len.ensure(c * 4));
+  LB_HIP(e->srch_pre.ensure((c + 1) * 4));
+  LB_HIP(e->srch_S.ensure(c * sizeof(g2j)));
+  LB_HIP(e->srch_pk.ensure(c * sizeof(g1j)));
+  LB_HIP(e->srch_verdict.ensure(c * 4));
+  LB_HIP(e->bcnt.ensure((size_t)nb * 4));
+  LB_HIP(e->bcursor.ensure((size_t)nb * 4));
+  LB_HIP(e->boff.ensure((size_t)(nb + 1) * 4));
+  LB_HIP(e->bch.ensure((size_t)(nb + 1) * 4));
+  LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
+  LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
+  LB_HIP(e->bmembers.ensure((size_t)2 * LB_MSM_W * (T ? T : 1) * 4));
+  LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
+  LB_HIP(e->bsum.ensure((size_t)nb * sizeof(g2j)));
+  LB_HIP(hipMemcpyAsync(e->srch_kind.p, hk.data(), c * 4, hipMemcpyHostToDevice, s1));
+  LB_HIP(hipMemcpyAsync(e->srch_key.p, hkey.data(), c * 4, hipMemcpyHostToDevice, s1));
+  LB_HIP(hipMemcpyAsync(e->srch_lo.p, hlo.data(), c * 4, hipMemcpyHostToDevice, s1));
+  LB_HIP(hipMemcpyAsync(e->srch_len.p, hlen.data(), c * 4, hipMemcpyHostToDevice, s1));
+  LB_HIP(hipMemcpyAsync(e->srch_pre.p, pre.data(), (c + 1) * 4, hipMemcpyHostToDevice, s1));
+  {
+    stage_scope sc(e, ST_FALLBACK, s1);
+    // S_j by one range MSM over all nodes of this round
+    LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)nb * 4, s1));
+    LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)nb * 4, s1));
+    hipLaunchKernelGGL(k_rmsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, (uint32_t)c, e->srch_pre.as<uint32_t>(),
+                       e->srch_lo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                       e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+    hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
+                       e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
+                       e->bchunk_end.as<uint32_t>());
+    hipLaunchKernelGGL(k_rmsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, (uint32_t)c,
+                       e->srch_pre.as<uint32_t>(), e->srch_lo.as<uint32_t>(), e->members.as<uint32_t>(),
+                       e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                       e->boff.as<uint32_t>(), e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
+                       e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
+                       e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
+    hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
+                       e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
+    hipLaunchKernelGGL(k_msm_reduce, dim3((uint32_t)c), dim3(64), 0, s1, e->bsum.as<uint32_t>(), nb,
+                       e->srch_S.as<uint32_t>(), (uint32_t)c, 0u);
+    // kind-1 nodes: sum r_i PK_i over the part
+    hipLaunchKernelGGL(k_range_pk, dim3(nblk((uint32_t)c)), dim3(LB_TPB), 0, s1, (uint32_t)c,
+                       e->srch_kind.as<uint32_t>(), e->srch_lo.as<uint32_t>(), e->srch_len.as<uint32_t>(),
+                       e->members.as<uint32_t>(), e->set_live.as<uint32_t>(), n, e->rpk.as<uint32_t>(),
+                       e->srch_pk.as<uint32_t>());
+  }
+  {
+    stage_scope sc(e, ST_BISECT, s1);
+    hipLaunchKernelGGL(k_search_check, dim3((uint32_t)c), dim3(64), 0, s1, (uint32_t)c, e->srch_kind.as<uint32_t>(),
+                       e->srch_key.as<uint32_t>(), e->treeP.as<uint32_t>(), 2 * mu, e->srch_pk.as<uint32_t>(),
+                       e->h_aff.as<uint32_t>(), n, e->srch_S.as<uint32_t>(), e->srch_verdict.as<int32_t>());
+  }
   LB_HIP(hipGetLastError());
+  verdict.resize(c);
+  LB_HIP(hipMemcpyAsync(verdict.data(), e->srch_verdict.p, c * 4, hipMemcpyDeviceToHost, s1));
+  LB_HIP(hipStreamSynchronize(s1));
   return LB_OK;
 }
 
-static int32_t check_nodes(lb_engine* e, uint32_t m, const std::vector<uint32_t>& nodes, std::vector<int32_t>& v) {
-  uint32_t c = (uint32_t)nodes.size();
-  v.assign(c, 0);
-  if (!c) return LB_OK;
-  LB_HIP(e->nodes.ensure((size_t)c * 4));
-  LB_HIP(e->verdict.ensure((size_t)c * 4));
-  LB_HIP(hipMemcpyAsync(e->nodes.p, nodes.data(), (size_t)c * 4, hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_node_check, dim3(c), dim3(64), 0, e->stream, m, c, e->nodes.as<uint32_t>(),
-                     e->treeP.as<uint32_t>(), e->treeS.as<uint32_t>(), e->verdict.as<int32_t>());
-  LB_HIP(hipGetLastError());
-  LB_HIP(hipMemcpyAsync(v.data(), e->verdict.p, (size_t)c * 4, hipMemcpyDeviceToHost, e->stream));
+// Refines a failing node into its children (appended to `out`); a single failing set goes to
+// `bad_pos` (its position in the members array).
+static void refine(const search_node& f, int32_t fid, uint32_t L, uint32_t nu, const std::vector<uint32_t>& goff,
+                   uint32_t tree_step, std::vector<search_node>& out, std::vector<uint32_t>& bad_pos) {
+  const uint32_t mu = 1u << L;
+  if (f.kind == 0) {
+    uint32_t d = 0;
+    while ((2u << d) <= f.key) d++;  // depth of heap index key
+    if (d == L) {  // a leaf: root u's members, in up to 64 parts
+      const uint32_t u = f.key - mu, lo = goff[u], len = goff[u + 1] - goff[u];
+      if (len == 1) {
+        bad_pos.push_back(lo);
+        return;
+      }
+      const uint32_t parts = len < 64 ? len : 64, per = (len + parts - 1) / parts;
+      for (uint32_t a = 0; a < len; a += per)
+        out.push_back({1u, u, lo + a, (a + per < len ? per : len - a), fid});
+      return;
+    }
+    const uint32_t dd = d + tree_step < L ? d + tree_step : L, k = dd - d;
+    for (uint32_t v = f.key << k; v < (f.key + 1) << k; v++) {
+      const uint32_t span = L - dd, ulo = (v - (1u << dd)) << span;
+      if (ulo >= nu) break;
+      const uint32_t uhi = (((v - (1u << dd)) + 1) << span) < nu ? (((v - (1u << dd)) + 1) << span) : nu;
+      out.push_back({0u, v, goff[ulo], goff[uhi] - goff[ulo], fid});
+    }
+    return;
+  }
+  if (f.len == 1) {
+    bad_pos.push_back(f.lo);
+    return;
+  }
+  const uint32_t parts = f.len < 64 ? f.len : 64, per = (f.len + parts - 1) / parts;
+  for (uint32_t a = 0; a < f.len; a += per) out.push_back({1u, f.key, f.lo + a, (a + per < f.len ? per : f.len - a), fid});
+}
+
+static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* out_job) {
+  const uint32_t n = b->n_sets, nj = b->n_jobs;
+  uint32_t L = 0;
+  while ((1u << L) < mu) L++;
+  const uint32_t nu = *e->h_nu;
+  std::vector<uint32_t> goff(nu + 1), members(n);
+  LB_HIP(hipMemcpyAsync(goff.data(), e->goff.p, (size_t)(nu + 1) * 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipMemcpyAsync(members.data(), e->members.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipStreamSynchronize(e->stream));
+  std::vector<search_node> failing{{0u, 1u, 0u, n, -1}};  // the root: known to fail
+  std::vector<uint32_t> bad_pos;
+  const size_t kMaxNodes = 256;
+  bool first = true;
+  while (!failing.empty()) {
+    std::vector<search_node> cand;
+    for (size_t k = 0; k < failing.size(); k++) refine(failing[k], (int32_t)k, L, nu, goff, first ? 8 : 6, cand, bad_pos);
+    first = false;
+    if (cand.empty()) break;
+    std::vector<int32_t> v(cand.size()), vk;
+    for (size_t a = 0; a < cand.size(); a += kMaxNodes) {
+      const size_t c = cand.size() - a < kMaxNodes ? cand.size() - a : kMaxNodes;
+      int32_t st = check_search_nodes(e, cand, a, c, n, mu, vk);
+      if (st != LB_OK) return st;
+      for (size_t j = 0; j < c; j++) v[a + j] = vk[j];
+    }
+    // fail closed: a failing node none of whose children fails (impossible for exact arithmetic)
+    // condemns its whole range
+    std::vector<int> child_fail(failing.size(), 0);
+    std::vector<search_node> next;
+    for (size_t j = 0; j < cand.size(); j++)
+      if (!v[j]) {
+        child_fail[cand[j].parent]++;
+        next.push_back(cand[j]);
+      }
+    for (size_t k = 0; k < failing.size(); k++) {
+      bool refined = false;
+      for (const search_node& c2 : cand) refined |= c2.parent == (int32_t)k;
+      if (refined && !child_fail[k])
+        for (uint32_t q = 0; q < failing[k].len; q++) bad_pos.push_back(failing[k].lo + q);
+    }
+    failing.swap(next);
+  }
+  // failing sets -> their jobs (set_live makes every failing set belong to a live job)
+  for (uint32_t pos : bad_pos) {
+    const uint32_t i = members[pos];
+    const uint32_t j = (uint32_t)(std::upper_bound(b->job_off.begin(), b->job_off.end(), i) - b->job_off.begin()) - 1;
+    if (j < nj && out_job[j] == 1) out_job[j] = 0;
+  }
   return LB_OK;
 }
 
@@ -761,65 +900,14 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   LB_HIP(hipMemcpyAsync(jst.data(), e->job_status.p, (size_t)nj * 4, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipMemcpyAsync(&root_ok, e->verdict.p, 4, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipStreamSynchronize(e->stream));
-  // subtree "live job" counts, heap layout (leaves at [m, 2m))
-  std::vector<uint32_t> live(2 * m, 0);
-  for (uint32_t j = 0; j < nj; j++) live[m + j] = jst[j] == LB_OK ? 1u : 0u;
-  for (uint32_t i = m - 1; i >= 1; i--) live[i] = live[2 * i] + live[2 * i + 1];
-  for (uint32_t j = 0; j < nj; j++) out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
-  // bisection over the job tree below a failing root
-  std::vector<uint32_t> cand;
-  std::vector<int32_t> v;
-  if (live[1] && !root_ok) {
-    if (m == 1) {
-      out_job[0] = 0;
-    } else {
-      // the job tree's root is the same product as the failed message tree's: start below it
-      st = run_fallback(e, b, m);
-      if (st != LB_OK) return st;
-      cand.push_back(2);
-      cand.push_back(3);
-    }
+  bool any_live = false;
+  for (uint32_t j = 0; j < nj; j++) {
+    out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
+    any_live |= jst[j] == LB_OK;
   }
-  {
-    stage_scope sc(e, ST_BISECT, e->stream);
-    while (!cand.empty()) {
-      // drop empty subtrees; when the failing subtrees are small, test their leaves directly
-      std::vector<uint32_t> nz;
-      uint64_t leaves = 0;
-      for (uint32_t c : cand)
-        if (live[c]) {
-          nz.push_back(c);
-          leaves += live[c];
-        }
-      if (!nz.empty() && leaves <= 256) {
-        std::vector<uint32_t> lv;
-        for (uint32_t c : nz) {
-          uint32_t lo = c, hi = c;
-          while (lo < m) {
-            lo = 2 * lo;
-            hi = 2 * hi + 1;
-          }
-          for (uint32_t l = lo; l <= hi; l++)
-            if (live[l]) lv.push_back(l);
-        }
-        nz.swap(lv);
-      }
-      if (nz.empty()) break;
-      st = check_nodes(e, m, nz, v);
-      if (st != LB_OK) return st;
-      std::vector<uint32_t> next;
-      for (size_t k = 0; k < nz.size(); k++) {
-        uint32_t c = nz[k];
-        if (v[k]) continue;  // verified: its live jobs stay 1
-        if (c >= m) {
-          out_job[c - m] = 0;
-          continue;
-        }
-        next.push_back(2 * c);
-        next.push_back(2 * c + 1);
-      }
-      cand.swap(next);
-    }
+  if (any_live && !root_ok) {
+    st = search_invalid(e, b, mu, out_job);
+    if (st != LB_OK) return st;
   }
   if (e->profiling) hipEventRecord(e->ev1[ST_TOTAL], e->stream);
   finish_profile(e);

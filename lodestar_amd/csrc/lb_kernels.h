@@ -2,14 +2,17 @@
 //
 // Pipeline for one batch of jobs (blst semantics of
 // Pairing.mul_n_aggregate + commit + finalverify behind maybeBatch.ts:18-25):
-//   k_decode_sigs     per set   : compressed G2 -> affine + subgroup check   (Signature.fromBytes(.., true))
-//   k_hash_map        per set x2: expand_message_xmd + SSWU + 3-isogeny      (hash_to_G2, first half)
-//   k_hash_finish     per set   : Q0 + Q1, clear cofactor, to affine          (hash_to_G2, second half)
-//   k_pk_blind        per set   : G1 aggregation (utils.ts:5-16), r*PK, r*sig
-//   k_miller          per set   : ML(r*PK, H(m))                               (Pairing.mul_n_aggregate)
-//   k_job_leaves      per job   : P_j = prod ML, S_j = sum r*sig -> tree leaves
-//   k_tree_up         per node  : product tree over jobs (bisection structure)
-//   k_node_check      per node  : FE(P * ML(-G1, S)) == 1                      (Pairing.finalverify)
+//   k_decompress_sigs / k_sig_subgroup   per set : compressed G2 -> affine, psi subgroup check
+//                                                   (Signature.fromBytes(.., true))
+//   k_msg_*            per set   : group the sets by signing root (hash table, counting sort)
+//   k_hash_map         per root x2: expand_message_xmd + SSWU + 3-isogeny     (hash_to_G2, first half)
+//   k_hash_finish      per root  : Q0 + Q1, clear cofactor, to affine        (hash_to_G2, second half)
+//   k_pk_chunks[_idx] / k_pk_blind per set: G1 aggregation (utils.ts:5-16), r*PK
+//   k_gsum_*           per root  : P_u = sum r_i PK_i over the root's live sets
+//   k_miller_grouped   per root  : ML(P_u, H(m_u))                         (Pairing.mul_n_aggregate)
+//   k_msm_*            per set   : S = sum r_i sig_i (bucket MSM)
+//   k_tree_up_U / k_ml_S / k_root_check : product tree, ML(-G1, S), one final exponentiation
+//   k_rmsm_*, k_range_pk, k_search_check : the invalid-set search after a failing root
 // All intermediate arrays are structure-of-arrays, word-major: word w of element e lives at
 // base[w * n + e], so a wave's 64 lanes touch 64 consecutive words per access.
 #pragma once
@@ -401,49 +404,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   pk_status[i] = st;
 }
 
-// r * sig (Jacobian G2) for the aggregate-signature side of the batch equation
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_blind(uint32_t n, const uint64_t* __restrict__ scalars,
-                                                      const uint32_t* __restrict__ sig_aff,
-                                                      const uint32_t* __restrict__ sig_inf,
-                                                      const int32_t* __restrict__ sig_status,
-                                                      uint32_t* __restrict__ rsig) {
-  uint32_t i = lb_tid();
-  if (i >= n) return;
-  g2j rs = jac_infinity<fp2>();
-  if (sig_status[i] == LB_OK && sig_inf[i] == 0u) {
-    // r * sig with r = lo + hi * lambda (k_pk_blind): [lambda]sig = -psi^2(sig) and
-    // sig + [lambda]sig = -psi^4(sig) on G2 (decoded signatures are subgroup-checked)
-    const g2a s = soa_ld<g2a>(sig_aff, n, i);
-    const g2a t2{fp2_mul_fp(s.x, fp_load(LB_PSI2_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI2_CY)))};
-    const g2a t3{fp2_mul_fp(s.x, fp_load(LB_PSI4_CX)), fp2_neg(fp2_mul_fp(s.y, fp_load(LB_PSI4_CY)))};
-    rs = jac_mul_glv(s, t2, t3, scalars[i]);
-  }
-  soa_st(rsig, n, i, rs);
-}
-
 // ---------------------------------------------------------------- Miller loops
-// Per-set loops ML(r_i PK_i, H(m_i)): only the fallback after a failing grouped root needs them
-// (per-job bisection).  H(m_i) is the hash of the set's unique message (set_uid).
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller(uint32_t n, const uint32_t* __restrict__ rpk,
-                                                   const uint32_t* __restrict__ h_aff,
-                                                   const uint32_t* __restrict__ set_uid,
-                                                   const int32_t* __restrict__ pk_status,
-                                                   uint32_t* __restrict__ ml) {
-  uint32_t i = lb_tid();
-  if (i >= n) return;
-  fp12 f = fp12_one();
-  if (pk_status[i] == LB_OK) {
-    const g1j pj = soa_ld<g1j>(rpk, n, i);
-    if (!jac_is_inf(pj)) {  // r*PK at infinity: ML = 1
-      g1a p;
-      jac_to_aff(p, pj);
-      g2a h = soa_ld<g2a>(h_aff, n, set_uid[i]);
-      f = miller_loop_inl(p, h);
-    }
-  }
-  soa_st(ml, n, i, f);
-}
-
 // Grouped loops: ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u
 // (bilinearity: prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into
 // leaf m + u of the message product tree (stride 2m).  Lanes u >= *n_u are idle.
@@ -588,8 +549,8 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32
 // joins bucket (window, d); bucket sums come from chunked Jacobian sums of the members (the
 // message-grouping machinery: count, k_msg_scan, scatter, chunks); one wave then forms
 // sum_d d B_d per window and combines the windows.  About 8 mixed additions per set instead of
-// the 32 doublings + 32 additions of a per-set r*sig; the per-set products (k_sig_blind) are
-// only computed by the fallback, whose bisection needs per-job sums.
+// the 32 doublings + 32 additions of a per-set r*sig.  The invalid-set search reuses the same
+// machinery over ranges of sets (k_rmsm_*) after a failing root check.
 #define LB_MSM_C 8
 #define LB_MSM_W 4
 #define LB_MSM_B (1 << LB_MSM_C)
@@ -631,15 +592,15 @@ __global__ void __launch_bounds__(LB_TPB) k_msm_scatter(uint32_t n, const uint64
   }
 }
 // chunk c of a bucket: Jacobian sum of its member points (AoS affine signatures; bit 31 of a
-// member = the [lambda] image)
+// member = the [lambda] image).  nb = bucket count (bch has nb + 1 entries).
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32_t* __restrict__ bch,
                                                        const uint32_t* __restrict__ chunk_beg,
                                                        const uint32_t* __restrict__ chunk_end,
                                                        const uint32_t* __restrict__ members,
                                                        const uint4* __restrict__ sig_aos, uint32_t cap,
-                                                       uint32_t* __restrict__ bacc) {
+                                                       uint32_t* __restrict__ bacc, uint32_t nb) {
   const uint32_t c = lb_tid();
-  if (c >= bch[LB_MSM_NB]) return;
+  if (c >= bch[nb]) return;
   g2j acc = jac_infinity<fp2>();
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t m = members[k], i = m & 0x7fffffffu;
@@ -660,31 +621,32 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32
   }
   soa_st(bacc, cap, c, acc);
 }
-// bucket b = sum of its chunk sums (SoA, stride LB_MSM_NB); empty buckets are infinity
+// bucket b = sum of its chunk sums (SoA, stride nb); empty buckets are infinity
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t* __restrict__ bch,
                                                         const uint32_t* __restrict__ bacc, uint32_t cap,
-                                                        uint32_t* __restrict__ bsum) {
+                                                        uint32_t* __restrict__ bsum, uint32_t nb) {
   const uint32_t b = lb_tid();
-  if (b >= LB_MSM_NB) return;
+  if (b >= nb) return;
   g2j acc = jac_infinity<fp2>();
   for (uint32_t c = bch[b]; c < bch[b + 1]; c++) acc = jac_add_i(acc, soa_ld<g2j>(bacc, cap, c));
-  soa_st(bsum, LB_MSM_NB, b, acc);
+  soa_st(bsum, nb, b, acc);
 }
-// One wave: lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
+// One wave per MSM instance j (buckets [j LB_MSM_NB, (j+1) LB_MSM_NB) of bsum, stride nb):
+// lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
 // Y = sum_j j B_{16s+j} and T = sum_j B_{16s+j}; Y + 16 s T is the segment's share of
 // sum_d d B_d.  Segments then add up in an LDS tree, and the windows combine Horner-style:
-// S = sum_w 2^(8w) W_w  -> treeS node 1 (stride n2m), where k_ml_S reads S_root.
-__global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t n2m,
-                                                   uint32_t* __restrict__ treeS) {
+// S = sum_w 2^(8w) W_w  -> element out0 + j of `out` (SoA, stride n_out).
+__global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                   uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
   static_assert(LB_MSM_W * 16 == 64 && LB_MSM_B == 256, "one lane per 16-digit segment");
   __shared__ g2j sh[64];
-  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u;
+  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u, base = blockIdx.x * LB_MSM_NB;
   g2j run = jac_infinity<fp2>(), y = jac_infinity<fp2>();
   for (int j = 15; j >= 1; j--) {
-    run = jac_add_i(run, soa_ld<g2j>(bsum, LB_MSM_NB, w * LB_MSM_B + 16 * sg + j));
+    run = jac_add_i(run, soa_ld<g2j>(bsum, nb, base + w * LB_MSM_B + 16 * sg + j));
     y = jac_add_i(y, run);
   }
-  if (sg) run = jac_add_i(run, soa_ld<g2j>(bsum, LB_MSM_NB, w * LB_MSM_B + 16 * sg));
+  if (sg) run = jac_add_i(run, soa_ld<g2j>(bsum, nb, base + w * LB_MSM_B + 16 * sg));
   // y += 16 sg * run   (sg < 16: 4-bit double-and-add, then 4 doublings)
   g2j t = jac_infinity<fp2>();
   for (int b = 3; b >= 0; b--) {
@@ -705,8 +667,153 @@ __global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ 
       for (int b = 0; b < LB_MSM_C; b++) S = jac_dbl_i(S);
       S = jac_add_i(S, sh[16 * ww]);
     }
-    soa_st(treeS, n2m, 1, S);
+    soa_st(out, n_out, out0 + blockIdx.x, S);
   }
+}
+
+// ---------------------------------------------------------------- invalid-set search
+// After a failing root check the engine searches for the failing sets over NODES: a node is a
+// contiguous range [lo_j, lo_j + len_j) of the members array (sets sorted by signing root) and
+// passes iff FE(P_j * ML(-G1, S_j)) == 1 with S_j = sum r_i sig_i over its live sets and
+//   kind 0 (a subtree of the root product tree, whole roots): P_j = treeP[v_j];
+//   kind 1 (part of one root u_j's members): P_j = ML(sum r_i PK_i, H(m_u)).
+// By bilinearity a node's verdict is the product of its children's, so a failing node has a
+// failing child; the host descends until single sets (lb_engine.hip search_invalid).
+// Range MSM for S_j: every (set, window) digit of node j joins bucket j LB_MSM_NB + w 256 + d.
+// Thread t of the T = sum len_j member positions finds its node by binary search of pre[].
+__device__ __forceinline__ uint32_t rmsm_node(const uint32_t* __restrict__ pre, uint32_t c, uint32_t t) {
+  uint32_t lo = 0, hi = c;  // pre[lo] <= t < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= t) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+__global__ void __launch_bounds__(LB_TPB) k_rmsm_count(uint32_t T, uint32_t c, const uint32_t* __restrict__ pre,
+                                                       const uint32_t* __restrict__ rlo,
+                                                       const uint32_t* __restrict__ members,
+                                                       const uint64_t* __restrict__ scalars,
+                                                       const uint32_t* __restrict__ set_live,
+                                                       const uint32_t* __restrict__ sig_inf,
+                                                       uint32_t* __restrict__ cnt) {
+  const uint32_t t = lb_tid();
+  if (t >= T) return;
+  const uint32_t j = rmsm_node(pre, c, t), i = members[rlo[j] + t - pre[j]];
+  if (!msm_live(i, set_live, sig_inf)) return;
+  const uint64_t wd = scalars[i];
+  LB_UNROLL for (int h = 0; h < 2; h++) {
+    const uint32_t k = (uint32_t)(wd >> (32 * h));
+    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
+      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+      if (d) atomicAdd(&cnt[j * LB_MSM_NB + w * LB_MSM_B + d], 1u);
+    }
+  }
+}
+__global__ void __launch_bounds__(LB_TPB) k_rmsm_scatter(uint32_t T, uint32_t c, const uint32_t* __restrict__ pre,
+                                                         const uint32_t* __restrict__ rlo,
+                                                         const uint32_t* __restrict__ members,
+                                                         const uint64_t* __restrict__ scalars,
+                                                         const uint32_t* __restrict__ set_live,
+                                                         const uint32_t* __restrict__ sig_inf,
+                                                         const uint32_t* __restrict__ boff,
+                                                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ bmembers) {
+  const uint32_t t = lb_tid();
+  if (t >= T) return;
+  const uint32_t j = rmsm_node(pre, c, t), i = members[rlo[j] + t - pre[j]];
+  if (!msm_live(i, set_live, sig_inf)) return;
+  const uint64_t wd = scalars[i];
+  LB_UNROLL for (int h = 0; h < 2; h++) {
+    const uint32_t k = (uint32_t)(wd >> (32 * h));
+    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
+      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+      if (d) {
+        const uint32_t b = j * LB_MSM_NB + w * LB_MSM_B + d;
+        bmembers[boff[b] + atomicAdd(&cursor[b], 1u)] = i | ((uint32_t)h << 31);
+      }
+    }
+  }
+}
+// kind-1 nodes: Jacobian sum of r_i PK_i over the node's live members -> pk_out (SoA, stride c)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,
+                                                       const uint32_t* __restrict__ rlo,
+                                                       const uint32_t* __restrict__ rlen,
+                                                       const uint32_t* __restrict__ members,
+                                                       const uint32_t* __restrict__ set_live, uint32_t n,
+                                                       const uint32_t* __restrict__ rpk, uint32_t* __restrict__ pk_out) {
+  const uint32_t j = lb_tid();
+  if (j >= c || kind[j] != 1u) return;
+  g1j acc = jac_infinity<fp>();
+  for (uint32_t k = rlo[j]; k < rlo[j] + rlen[j]; k++) {
+    const uint32_t i = members[k];
+    if (set_live[i]) acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));
+  }
+  soa_st(pk_out, c, j, acc);
+}
+// One wave per node: verdict[j] = FE(P_j * ML(-G1, S_j)) == 1 (Pairing.finalverify)
+__global__ void __launch_bounds__(64) k_search_check(uint32_t c, const uint32_t* __restrict__ kind,
+                                                     const uint32_t* __restrict__ key,
+                                                     const uint32_t* __restrict__ treeP, uint32_t n2m,
+                                                     const uint32_t* __restrict__ pk_out,
+                                                     const uint32_t* __restrict__ h_aff, uint32_t n,
+                                                     const uint32_t* __restrict__ s_out,
+                                                     int32_t* __restrict__ verdict) {
+  LBW_SHARED(S);
+  __shared__ int s_inf;
+  const uint32_t j = blockIdx.x;
+  if (j >= c) return;
+  const int lane = threadIdx.x;
+  w_init_consts(S);
+  if (kind[j] == 0u) {
+    w_load_soa12(S, LBW_A(0), treeP, n2m, key[j]);
+  } else {
+    if (lane == 0) {
+      const g1j pj = soa_ld<g1j>(pk_out, c, j);
+      s_inf = jac_is_inf(pj) ? 1 : 0;
+      if (!s_inf) {
+        g1a pa;
+        jac_to_aff(pa, pj);
+        const g2a h = soa_ld<g2a>(h_aff, n, key[j]);
+        w_st(S, LBW_PT + 0, pa.x);
+        w_st(S, LBW_PT + 1, pa.y);
+        w_st(S, LBW_PT + 2, h.x.c0);
+        w_st(S, LBW_PT + 3, h.x.c1);
+        w_st(S, LBW_PT + 4, h.y.c0);
+        w_st(S, LBW_PT + 5, h.y.c1);
+      }
+    }
+    w_sync();
+    const int inf = s_inf;
+    w_sync();
+    if (inf)
+      w_set_one(S, LBW_A(0));
+    else
+      w_miller(S, LBW_A(0));
+  }
+  if (lane == 0) {
+    const g2j Sj = soa_ld<g2j>(s_out, c, j);
+    s_inf = jac_is_inf(Sj) ? 1 : 0;
+    if (!s_inf) {
+      g2a a;
+      jac_to_aff(a, Sj);
+      w_st(S, LBW_PT + 0, fp_load(LB_G1X));
+      w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
+      w_st(S, LBW_PT + 2, a.x.c0);
+      w_st(S, LBW_PT + 3, a.x.c1);
+      w_st(S, LBW_PT + 4, a.y.c0);
+      w_st(S, LBW_PT + 5, a.y.c1);
+    }
+  }
+  w_sync();
+  const int sinf = s_inf;
+  w_sync();
+  if (!sinf) {
+    w_miller(S, LBW_A(7));
+    w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
+  }
+  w_final_exp(S, LBW_A(0), LBW_A(0));
+  const bool one = w_is_one(S, LBW_A(0));
+  if (lane == 0) verdict[j] = one ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- per-job leaves
@@ -798,11 +905,11 @@ __global__ void __launch_bounds__(64) k_g2_set_inf(uint32_t* __restrict__ base, 
   if (threadIdx.x == 0) soa_st(base, n, e, jac_infinity<fp2>());
 }
 
-// Message product tree, one level: like k_tree_up_P, but only leaves [0, *n_u) exist.  A node
+// Message product tree, one level (one wave per node), over leaves [0, *n_u) only.  A node
 // whose leaf range starts at or past *n_u is never read; one whose right half does is a copy.
 __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const uint32_t* __restrict__ n_u,
                                                   uint32_t* __restrict__ treeP) {
-  __shared__ fp S[LBW_SLOTS];
+  LBW_SHARED(S);
   const uint32_t i = lo + blockIdx.x, span = m / lo, start = blockIdx.x * span, nu = *n_u;
   if (start >= nu) return;
   w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
@@ -813,70 +920,10 @@ __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const
   w_store_soa12(S, LBW_A(0), treeP, 2 * m, i);
 }
 
-// P_j = prod ML_i over the job's sets (identity for a rejecting job) -> treeP leaf m + j
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_job_leaves_P(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
-                                                         const uint32_t* __restrict__ job_off,
-                                                         const int32_t* __restrict__ sig_status,
-                                                         const int32_t* __restrict__ pk_status,
-                                                         const uint32_t* __restrict__ ml, uint32_t* __restrict__ treeP,
-                                                         int32_t* __restrict__ job_status) {
-  uint32_t j = lb_tid();
-  if (j >= m) return;
-  fp12 P = fp12_one();
-  if (j < n_jobs) {
-    uint32_t a = job_off[j], e = job_off[j + 1];
-    int st = job_status_of(a, e, sig_status, pk_status);
-    if (st == LB_OK)
-      for (uint32_t i = a; i < e; i++) {
-        fp12 f = soa_ld<fp12>(ml, n_sets, i);
-        P = (i == a) ? f : fp12_mul(P, f);
-      }
-    job_status[j] = st;
-  }
-  soa_st(treeP, 2 * m, m + j, P);
-}
-
-// S_j = sum r_i sig_i over the job's sets (identity for a rejecting job) -> treeS leaf m + j
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_job_leaves_S(uint32_t n_jobs, uint32_t n_sets, uint32_t m,
-                                                         const uint32_t* __restrict__ job_off,
-                                                         const int32_t* __restrict__ sig_status,
-                                                         const int32_t* __restrict__ pk_status,
-                                                         const uint32_t* __restrict__ rsig, uint32_t* __restrict__ treeS) {
-  uint32_t j = lb_tid();
-  if (j >= m) return;
-  g2j S = jac_infinity<fp2>();
-  if (j < n_jobs) {
-    uint32_t a = job_off[j], e = job_off[j + 1];
-    if (job_status_of(a, e, sig_status, pk_status) == LB_OK)
-      for (uint32_t i = a; i < e; i++) S = jac_add(S, soa_ld<g2j>(rsig, n_sets, i));
-  }
-  soa_st(treeS, 2 * m, m + j, S);
-}
-
-// Product tree over jobs, one level: nodes [lo, 2 lo), node i = node 2i (x) node 2i+1.
-// One wave per node multiplies the Fp12 children cooperatively (MUL12 program).
-__global__ void __launch_bounds__(64) k_tree_up_P(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeP) {
-  __shared__ fp S[LBW_SLOTS];
-  uint32_t i = lo + blockIdx.x;
-  w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
-  w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
-  w_mul(S, LBW_A(2), LBW_A(0), LBW_A(1));
-  w_store_soa12(S, LBW_A(2), treeP, 2 * m, i);
-}
-
-// G2 sum tree, one level, one lane per node (Jacobian additions)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_tree_up_S(uint32_t m, uint32_t lo, uint32_t* __restrict__ treeS) {
-  uint32_t t = lb_tid();
-  if (t >= lo) return;
-  uint32_t i = lo + t;
-  g2j s = jac_add(soa_ld<g2j>(treeS, 2 * m, 2 * i), soa_ld<g2j>(treeS, 2 * m, 2 * i + 1));
-  soa_st(treeS, 2 * m, i, s);
-}
-
 // fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
 // computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
 __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
-  __shared__ fp S[LBW_SLOTS];
+  LBW_SHARED(S);
   __shared__ int s_inf;
   const int lane = threadIdx.x;
   w_init_consts(S);
@@ -886,12 +933,12 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
     if (!s_inf) {
       g2a a;
       jac_to_aff(a, Sj);
-      S[LBW_PT + 0] = fp_load(LB_G1X);
-      S[LBW_PT + 1] = fp_load(LB_G1NEGY);
-      S[LBW_PT + 2] = a.x.c0;
-      S[LBW_PT + 3] = a.x.c1;
-      S[LBW_PT + 4] = a.y.c0;
-      S[LBW_PT + 5] = a.y.c1;
+      w_st(S, LBW_PT + 0, fp_load(LB_G1X));
+      w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
+      w_st(S, LBW_PT + 2, a.x.c0);
+      w_st(S, LBW_PT + 3, a.x.c1);
+      w_st(S, LBW_PT + 4, a.y.c0);
+      w_st(S, LBW_PT + 5, a.y.c1);
     }
   }
   w_sync();
@@ -905,7 +952,7 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
 // root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
 __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
                                                    const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict) {
-  __shared__ fp S[LBW_SLOTS];
+  LBW_SHARED(S);
   w_init_consts(S);
   w_load_soa12(S, LBW_A(0), treeP, 2 * m, 1);
   w_load_soa12(S, LBW_A(7), fS, 1, 0);
@@ -915,33 +962,20 @@ __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* _
   if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
 
-// One wave per checked node: verdict = FE(P * ML(-G1, S)) == 1   (Pairing.finalverify)
-__global__ void __launch_bounds__(64) k_node_check(uint32_t m, uint32_t cnt, const uint32_t* __restrict__ nodes,
-                                                   const uint32_t* __restrict__ treeP,
-                                                   const uint32_t* __restrict__ treeS, int32_t* __restrict__ verdict) {
-  __shared__ fp S[LBW_SLOTS];
-  if (blockIdx.x >= cnt) return;
-  w_init_consts(S);
-  w_node_partial(S, LBW_A(0), treeP, treeS, 2 * m, nodes[blockIdx.x]);
-  w_final_exp(S, LBW_A(0), LBW_A(0));
-  bool one = w_is_one(S, LBW_A(0));
-  if (threadIdx.x == 0) verdict[blockIdx.x] = one ? 1 : 0;
-}
-
 // root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
 __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
                                                      const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
-  __shared__ fp S[LBW_SLOTS];
+  LBW_SHARED(S);
   w_init_consts(S);
   w_load_soa12(S, LBW_A(0), treeP, 2 * m, 1);
   w_load_soa12(S, LBW_A(7), fS, 1, 0);
   w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
-  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(S[LBW_A(0) + threadIdx.x]));
+  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(w_ld(S, LBW_A(0) + threadIdx.x)));
 }
 
 __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
                                                        int32_t* __restrict__ ok) {
-  __shared__ fp S[LBW_SLOTS];
+  LBW_SHARED(S);
   __shared__ int bad;
   const int lane = threadIdx.x;
   if (lane == 0) bad = 0;
@@ -951,7 +985,7 @@ __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t
     if (lane < 12) {
       fp x;
       if (!fp_plain_from_be48(x, parts + (size_t)576 * i + 48 * lane, 0xff)) atomicOr(&bad, 1);
-      S[LBW_A(7) + lane] = fp_to_mont(x);
+      w_st(S, LBW_A(7) + lane, fp_to_mont(x));
     }
     w_sync();
     w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));

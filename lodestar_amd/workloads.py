@@ -252,3 +252,15 @@ def indexed_for(engine: Engine, wl: Workload) -> PackedJobs:
     p = wl.packed
     return PackedJobs(job_off=p.job_off, pk_off=p.pk_off, pubkeys=None, msgs=p.msgs, sigs=p.sigs,
                       sig_sizes=p.sig_sizes, pk_indices=(p.pk_indices + np.uint32(base)).astype(np.uint32))
+
+
+def slice_jobs(p: PackedJobs, j0: int, j1: int) -> PackedJobs:
+    """Jobs [j0, j1) of a packed batch as their own batch (a rank's shard, distributed.shard_jobs)."""
+    s0, s1 = int(p.job_off[j0]), int(p.job_off[j1])
+    k0, k1 = int(p.pk_off[s0]), int(p.pk_off[s1])
+    return PackedJobs(job_off=(p.job_off[j0:j1 + 1] - s0).astype(np.uint32),
+                      pk_off=(p.pk_off[s0:s1 + 1] - k0).astype(np.uint32),
+                      pubkeys=None if p.pubkeys is None else p.pubkeys[96 * k0:96 * k1].copy(),
+                      msgs=p.msgs[32 * s0:32 * s1].copy(), sigs=p.sigs[96 * s0:96 * s1].copy(),
+                      sig_sizes=None if p.sig_sizes is None else p.sig_sizes[s0:s1].copy(),
+                      pk_indices=None if p.pk_indices is None else p.pk_indices[k0:k1].copy())

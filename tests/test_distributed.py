@@ -1,5 +1,6 @@
-"""World-size-2 gloo run of the multi-GPU exchange protocol (lodestar_amd/distributed.py) on CPU,
-with the CPU counterparts of lb_batch_partial / lb_fp12_product_is_one (oracle/cpu_pool.cpp)."""
+"""World-size-2 gloo runs of the multi-GPU exchange protocol (lodestar_amd/distributed.py): on CPU
+with the CPU counterparts of lb_batch_partial / lb_fp12_product_is_one (oracle/cpu_pool.cpp), and
+on the GPU box with two ranks sharing device 0, whose partials come from lb_batch_partial."""
 import ctypes
 import os
 import socket
@@ -99,3 +100,62 @@ def test_gloo_two_ranks_invalid_job_localised():
     assert oks == [False, False]
     _, exp = _jobs("batch_one_wrong")
     assert codes == _expected_codes(exp)
+
+
+def _worker_gpu(rank, world, port, name, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from lodestar_amd import workloads as W
+    from lodestar_amd.distributed import shard_jobs, verify_sharded
+    from lodestar_amd.engine import Engine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        wl = W.make(eng, name)          # deterministic: both ranks build the same workload
+        lo, hi = shard_jobs(wl.packed.n_jobs, world, rank)
+        shard = W.slice_jobs(wl.packed, lo, hi)
+        shard.pk_indices = None         # 96-byte keys
+        b = eng.upload(shard)
+        try:
+            codes, ok = verify_sharded(b.partial, eng.product_is_one, b.verify)
+        finally:
+            b.free()
+        out.put((rank, codes, ok, [int(x) for x in wl.expected[lo:hi]]))
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+def _run_gpu(name):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_gpu, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res)
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_gpu_partials_valid():
+    """c5 (32 block jobs) sharded over two ranks on device 0: lb_batch_partial partials, all-gather,
+    one final exponentiation of their product accepts everything."""
+    res = _run_gpu("c5")
+    assert [ok for _, _, ok, _ in res] == [True, True]
+    for _, codes, _, exp in res:
+        assert codes == exp == [1] * len(exp)
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_gpu_partials_invalid_localised():
+    """c4 carries wrong and malformed sets: the product check fails on both ranks and each rank's
+    own verify localises its invalid jobs."""
+    res = _run_gpu("c4")
+    assert [ok for _, _, ok, _ in res] == [False, False]
+    for _, codes, _, exp in res:
+        assert codes == exp

@@ -357,7 +357,7 @@ def test_shared_roots_grouped_path_accepts(engine):
     jobs = make_shared_batch(engine, 700, 5, agg_k=3, seed=21)
     codes, prof = _verify_profiled(engine, jobs)
     assert codes == [1] * 700
-    assert prof["fallback"] == 0.0 and prof["bisect"] >= 0.0
+    assert prof["search_msm"] == 0.0 and prof["search_check"] >= 0.0
 
 
 def test_shared_roots_invalid_member_found_by_fallback(engine):
@@ -366,7 +366,7 @@ def test_shared_roots_invalid_member_found_by_fallback(engine):
     codes, prof = _verify_profiled(engine, jobs)
     assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
     assert all(codes[i] == 0 for i in bad)
-    assert prof["fallback"] > 0.0
+    assert prof["search_msm"] > 0.0
 
 
 def test_shared_roots_malformed_job_excluded_without_fallback(engine):
@@ -379,7 +379,7 @@ def test_shared_roots_malformed_job_excluded_without_fallback(engine):
             assert N.error_name(-c) == "BLST_BAD_ENCODING"
         else:
             assert c == 1
-    assert prof["fallback"] == 0.0  # rejected jobs leave the per-root sums; the root still passes
+    assert prof["search_msm"] == 0.0  # rejected jobs leave the per-root sums; the root still passes
 
 
 def test_shared_roots_inside_one_job_and_duplicate_sets(engine):
@@ -405,7 +405,7 @@ def test_all_valid_distinct_roots_pass_at_the_root(engine):
     jobs = make_batch(engine, 300, agg_k=2, seed=27)
     codes, prof = _verify_profiled(engine, jobs)
     assert codes == [1] * 300
-    assert prof["fallback"] == 0.0
+    assert prof["search_msm"] == 0.0
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c4", "c5"])

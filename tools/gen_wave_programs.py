@@ -19,10 +19,14 @@ Slot map (per wave, in units of one Fp element = 12 u32):
   [64, ...) TEMP   products and materialised values; program outputs live here
 
 Encoding (int16): header [n_phases, n_temps, n_out, out_slot * n_out] padded to 8 entries,
-then per phase [kind, n_tasks, 0 x 6] + fixed-size records (PREC / LREC entries, 16-byte
-multiples, so a lane fetches its record with 16-byte vector loads); kind 0 = product phase,
-record [dst, (slot, coef) * MAXT for x, (slot, coef) * MAXT for y]; kind 1 = linear phase,
-record [dst, (slot, coef) * MAXL].  Terms are packed first; unused pairs have coef 0.
+then per phase a header [kind, n_tasks, npA, nnA, npB, nnB, redA, redB] + fixed-size records
+(PREC / LREC entries, 16-byte multiples, so a lane fetches its record with 16-byte vector
+loads); kind 0 = product phase, record [dst, (slot, coef) * MAXP for x, (slot, coef) * MAXP for
+y]; kind 1 = linear phase, record [dst, (slot, coef) * MAXL] (operand A only).  Within an
+operand the positive terms come first, padded to the phase-uniform count npA, then the negated
+ones (coefficients stored as magnitudes), padded to nnA; padding pairs have coefficient 0.  So every lane of a phase runs the same term loop with no sign branches.  red = B | (m << 8):
+the lazy sum is r = sum(pos) + 2^(m-1) p - sum(neg) < B p (m = 0: no negated terms), reduced
+by conditional subtraction of 2^j p for every 2^j < B.
 
 The program encoding is validated here by a Python interpreter against direct big-integer
 evaluation of the same tower formulas (and, through the engine tests, against the oracle).
@@ -33,13 +37,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
-MAXT = 8
-MAXL = 24
-PREC = 40   # product record: dst + 2 x 8 (slot, coef) pairs, padded to 16-byte multiple
-LREC = 56   # linear record: dst + 24 (slot, coef) pairs, padded
+MAXT = 8     # terms per product operand before the generator materialises it
+MAXL = 24    # terms per linear task
+MAXP = 10    # (slot, coef) pairs per product operand in a record (pos + neg, phase-uniform split)
+PREC = 48    # product record: dst + 2 x MAXP pairs, padded to a 16-byte multiple
+LREC = 56    # linear record: dst + MAXL pairs, padded
 IN_BASE, CONST_BASE, TEMP_BASE = 0, 32, 64
-C_B3, C_INV2, C_FROB1, C_FROB2 = 0, 2, 3, 13   # offsets in CONST
-N_CONST = 18
+C_B3, C_INV2, C_FROB1, C_FROB2, C_ZERO = 0, 2, 3, 13, 18   # offsets in CONST
+N_CONST = 19
 
 
 class Lin:
@@ -139,31 +144,51 @@ class Prog:
                 phases.append((1, [l for l in self.lins if l[0] == s and l[1] == v]))
         out = [len(phases), self.ntemp, len(self.outs)] + self.outs
         out += [0] * (-len(out) % 8)          # records start 16-byte aligned
+        pad = [IN_BASE, 0]   # padding pair: coefficient 0 (lb_wave.h skips it), any valid slot
+
+        def split(lin):
+            pos = [(sl, c) for sl, c in lin.d.items() if c > 0]
+            neg = [(sl, -c) for sl, c in lin.d.items() if c < 0]
+            assert all(c <= 7 for _, c in pos + neg)
+            return pos, neg
+
+        def red(ops):
+            psum = max(sum(c for _, c in p) for p, _ in ops)
+            nsum = max(sum(c for _, c in n) for _, n in ops)
+            m = 0
+            while nsum > ((1 << (m - 1)) if m else 0):
+                m += 1
+            bound = max(psum, 1) + ((1 << (m - 1)) if m else 0)
+            assert bound <= 128 and psum <= 64
+            return bound | (m << 8)
+
+        def pack(ops, np_, nn_, width):
+            rec = []
+            for p, n in [ops]:
+                for k in range(np_):
+                    rec += list(p[k]) if k < len(p) else pad
+                for k in range(nn_):
+                    rec += list(n[k]) if k < len(n) else pad
+            assert np_ + nn_ <= width
+            return rec + pad * (width - np_ - nn_)
+
         for kind, tasks in phases:
-            out += [kind, len(tasks)] + [0] * 6
-            for t in tasks:
-                if kind == 0:
-                    _, dst, x, y = t
-                    rec = [dst]
-                    for lin in (x, y):
-                        terms = list(lin.d.items())
-                        assert len(terms) <= MAXT
-                        assert sum(abs(c) for _, c in terms) <= 64  # lazy reduction bound (lb_wave.h)
-                        assert all(abs(c) <= 7 for _, c in terms)
-                        for k in range(MAXT):
-                            rec += list(terms[k]) if k < len(terms) else [0, 0]
-                    rec += [0] * (PREC - len(rec))
-                else:
-                    _, _, dst, lin = t
-                    terms = list(lin.d.items())
-                    assert len(terms) <= MAXL
-                    assert sum(abs(c) for _, c in terms) <= 64
-                    assert all(abs(c) <= 7 for _, c in terms)
-                    rec = [dst]
-                    for k in range(MAXL):
-                        rec += list(terms[k]) if k < len(terms) else [0, 0]
-                    rec += [0] * (LREC - len(rec))
-                out += rec
+            if kind == 0:
+                xs = [split(t[2]) for t in tasks]
+                ys = [split(t[3]) for t in tasks]
+                npa, nna = max(len(p) for p, _ in xs), max(len(n) for _, n in xs)
+                npb, nnb = max(len(p) for p, _ in ys), max(len(n) for _, n in ys)
+                out += [kind, len(tasks), npa, nna, npb, nnb, red(xs), red(ys)]
+                for t, x, y in zip(tasks, xs, ys):
+                    rec = [t[1]] + pack(x, npa, nna, MAXP) + pack(y, npb, nnb, MAXP)
+                    out += rec + [0] * (PREC - len(rec))
+            else:
+                ls = [split(t[3]) for t in tasks]
+                npa, nna = max(len(p) for p, _ in ls), max(len(n) for _, n in ls)
+                out += [kind, len(tasks), npa, nna, 0, 0, red(ls), 0]
+                for t, l in zip(tasks, ls):
+                    rec = [t[2]] + pack(l, npa, nna, MAXL)
+                    out += rec + [0] * (LREC - len(rec))
         for v in out:
             assert -32768 <= v < 32768
         return out
@@ -369,32 +394,37 @@ def build_programs():
 
 # ------------------------------------------------------------ reference evaluation (big ints)
 def run_encoded(code, slots):
-    """Interpret an encoded program over a dict slot -> int (mod P)."""
+    """Interpret an encoded program over a dict slot -> int (mod P), the way lb_wave.h does:
+    lazy positive / negated sums and the per-phase reduction bound are checked too."""
     n_ph, n_temp, n_out = code[0], code[1], code[2]
     outs = code[3:3 + n_out]
     pos = 3 + n_out
     pos += -pos % 8
     S = dict(slots)
 
-    def lin(rec, off, n):
-        acc = 0
-        for k in range(n):
-            s, c = rec[off + 2 * k], rec[off + 2 * k + 1]
-            if c:
-                acc += c * S[s]
-        return acc % P
+    def lin(rec, off, np_, nn_, red_):
+        bound, m = red_ & 0xFF, red_ >> 8
+        pa = sum(rec[off + 2 * k + 1] * S[rec[off + 2 * k]] for k in range(np_))
+        na = sum(rec[off + 2 * k + 1] * S[rec[off + 2 * k]] for k in range(np_, np_ + nn_))
+        r = pa + ((1 << (m - 1)) * P if m else 0) - na
+        assert 0 <= r < bound * P, "lazy reduction bound"
+        for j in range(6, -1, -1):
+            if (1 << j) < bound and r >= (1 << j) * P:
+                r -= (1 << j) * P
+        assert r < P
+        return r
 
     for _ in range(n_ph):
-        kind, n = code[pos], code[pos + 1]
+        kind, n, npa, nna, npb, nnb, ra, rb = code[pos:pos + 8]
         pos += 8
         rs = PREC if kind == 0 else LREC
         new = {}
         for k in range(n):
             rec = code[pos + k * rs: pos + (k + 1) * rs]
             if kind == 0:
-                new[rec[0]] = lin(rec, 1, MAXT) * lin(rec, 1 + 2 * MAXT, MAXT) % P
+                new[rec[0]] = lin(rec, 1, npa, nna, ra) * lin(rec, 1 + 2 * MAXP, npb, nnb, rb) % P
             else:
-                new[rec[0]] = lin(rec, 1, MAXL)
+                new[rec[0]] = lin(rec, 1, npa, nna, ra)
         S.update(new)
         pos += n * rs
     return [S[o] for o in outs]
@@ -467,11 +497,12 @@ def main():
     lines = ["// Generated by tools/gen_wave_programs.py -- do not edit.",
              "// Wave-cooperative programs (see the generator's docstring for the encoding).",
              "#pragma once", "#include <stdint.h>", "",
-             f"#define LBW_MAXT {MAXT}", f"#define LBW_MAXL {MAXL}", f"#define LBW_PREC {PREC}",
+             f"#define LBW_MAXT {MAXT}", f"#define LBW_MAXL {MAXL}", f"#define LBW_MAXP {MAXP}",
+             f"#define LBW_PREC {PREC}",
              f"#define LBW_LREC {LREC}",
              f"#define LBW_IN {IN_BASE}", f"#define LBW_CONST {CONST_BASE}", f"#define LBW_TEMP {TEMP_BASE}",
              f"#define LBW_C_B3 {C_B3}", f"#define LBW_C_INV2 {C_INV2}", f"#define LBW_C_FROB1 {C_FROB1}",
-             f"#define LBW_C_FROB2 {C_FROB2}", f"#define LBW_N_CONST {N_CONST}"]
+             f"#define LBW_C_FROB2 {C_FROB2}", f"#define LBW_C_ZERO {C_ZERO}", f"#define LBW_N_CONST {N_CONST}"]
     maxtemp = 0
     for name, code in codes.items():
         pg = progs[name]
