@@ -149,12 +149,35 @@ int32_t lb_aggregate_pubkeys(lb_engine* e, uint32_t n_sets, const uint32_t* set_
                              const uint8_t* pubkeys, uint8_t* out96, int32_t* out_status);
 
 /*
+ * G2 signature aggregation, bls.Signature.aggregate(sigs).toBytes() as the op pools use it for
+ * block production (beacon-node/src/chain/opPools/aggregatedAttestationPool.ts:321,
+ * attestationPool.ts:184, syncContributionAndProofPool.ts:185).
+ * Group g sums signatures [group_offsets[g], group_offsets[g+1]) of sigs96 (96 B compressed
+ * each; sig_sizes as in lb_batch_create, NULL = all 96); validate != 0 adds the G2 subgroup
+ * check of Signature.fromBytes(.., true).  out96[g] = compressed sum (infinity = 0xc0 || 0^95),
+ * out_status[g] = LB_OK, the first bad signature's decode error, or LB_EMPTY_AGGREGATE_ARRAY.
+ */
+int32_t lb_aggregate_signatures(lb_engine* e, uint32_t n_groups, const uint32_t* group_offsets,
+                                const uint8_t* sigs96, const uint32_t* sig_sizes, int32_t validate,
+                                uint8_t* out96, int32_t* out_status);
+
+/*
  * Batch G1 decompression (48 B compressed -> 96 B uncompressed), the pubkey cache's one-time
  * deserialisation (state-transition/src/cache/pubkeyCache.ts:56-77).  validate != 0 adds
  * PublicKey.keyValidate: infinity -> LB_PK_IS_INFINITY, not in G1 -> LB_POINT_NOT_IN_GROUP.
  */
 int32_t lb_g1_decompress(lb_engine* e, uint32_t n, const uint8_t* in48, uint8_t* out96, int32_t* out_status,
                          int32_t validate);
+
+/*
+ * SSZ merkleization (the hashing of signing-root production: getBlockSignatureSets ->
+ * computeSigningRoot, state-transition/src/signatureSets/index.ts:64-111, src/util/signingRoot.ts:7-13;
+ * SURVEY.md §8(f) row 2).  Tree t hashes chunks [chunk_offsets[t], chunk_offsets[t+1]) of
+ * chunks32 (32 B each) padded with zero chunks to 2^depths[t] leaves; mix_lengths[t] != UINT64_MAX
+ * mixes in that length (SSZ lists / bitlists).  out_roots32[t] = the 32-byte root.
+ */
+int32_t lb_merkleize(lb_engine* e, uint32_t n_trees, const uint32_t* chunk_offsets, const uint8_t* chunks32,
+                     const uint32_t* depths, const uint64_t* mix_lengths, uint8_t* out_roots32);
 
 /*
  * Synthetic-data helpers for tests and the benchmark (not on the verification path):

@@ -110,6 +110,8 @@ struct lb_engine {
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum;
   // invalid-set search (search_invalid): node descriptors and per-node results
   dbuf srch_kind, srch_key, srch_lo, srch_len, srch_pre, srch_S, srch_pk, srch_verdict;
+  dbuf pk_aff;  // affine aggregate pubkey per set (single-set checks of the search)
+  dbuf srch_midx, srch_mlo;
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -257,7 +259,8 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
                   &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->srch_kind, &e->srch_key,
-                  &e->srch_lo, &e->srch_len, &e->srch_pre, &e->srch_S, &e->srch_pk, &e->srch_verdict};
+                  &e->srch_lo, &e->srch_len, &e->srch_pre, &e->srch_S, &e->srch_pk, &e->srch_verdict,
+                  &e->pk_aff, &e->srch_midx, &e->srch_mlo};
   for (dbuf* b : bufs) b->release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
@@ -515,6 +518,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->q.ensure((size_t)ns * 2 * sizeof(g2j)));
   LB_HIP(e->h_aff.ensure((size_t)ns * sizeof(g2a)));
   LB_HIP(e->rpk.ensure((size_t)ns * sizeof(g1j)));
+  LB_HIP(e->pk_aff.ensure((size_t)ns * sizeof(g1a)));
   LB_HIP(e->pk_status.ensure((size_t)ns * 4));
   LB_HIP(e->treeP.ensure((size_t)2 * mt * sizeof(fp12)));
   LB_HIP(e->treeS.ensure((size_t)2 * mj * sizeof(g2j)));
@@ -570,7 +574,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     {
       stage_scope sc(e, ST_PK_BLIND, s2);
       hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s2, n, nc, b->d_set_chunk_off.as<uint32_t>(),
-                         e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), b->d_pk_off.as<uint32_t>(),
+                         e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
                          e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
     }
     // signatures: decoded while s1 groups and hashes the messages
@@ -699,7 +703,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
 // the range MSMs touch each member once per level it is under a failing node.
 namespace {
 struct search_node {
-  uint32_t kind, key, lo, len;  // kind 0: key = heap index in the root tree; 1: key = root id
+  uint32_t kind, key, lo, len;  // kind 0: key = heap index in the root tree; 1: key = root id;
+                                // 2: key = set index (one set, lo = its members position)
   int32_t parent;               // index of the failing node this one refines (-1: the root)
 };
 }  // namespace
@@ -707,61 +712,73 @@ struct search_node {
 static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& nd, size_t a, size_t c, uint32_t n,
                                   uint32_t mu, std::vector<int32_t>& verdict) {
   hipStream_t s1 = e->stream;
-  std::vector<uint32_t> hk(c), hkey(c), hlo(c), hlen(c), pre(c + 1);
-  pre[0] = 0;
+  // node arrays; the range MSM runs over the kind-0/1 nodes only (midx = their MSM instance)
+  std::vector<uint32_t> hk(c), hkey(c), hlo(c), hlen(c), midx(c), mlo, mpre{0};
   for (size_t j = 0; j < c; j++) {
-    hk[j] = nd[a + j].kind;
-    hkey[j] = nd[a + j].key;
-    hlo[j] = nd[a + j].lo;
-    hlen[j] = nd[a + j].len;
-    pre[j + 1] = pre[j] + hlen[j];
+    const search_node& x = nd[a + j];
+    hk[j] = x.kind;
+    hkey[j] = x.key;
+    hlo[j] = x.lo;
+    hlen[j] = x.len;
+    midx[j] = 0;
+    if (x.kind != 2u) {
+      midx[j] = (uint32_t)mlo.size();
+      mlo.push_back(x.lo);
+      mpre.push_back(mpre.back() + x.len);
+    }
   }
-  const uint32_t T = pre[c], nb = (uint32_t)c * LB_MSM_NB;
+  const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * LB_MSM_NB;
   const uint32_t bcap = (2 * LB_MSM_W * T) / LB_GROUP_CHUNK + nb;
   LB_HIP(e->srch_kind.ensure(c * 4));
   LB_HIP(e->srch_key.ensure(c * 4));
   LB_HIP(e->srch_lo.ensure(c * 4));
   LB_HIP(e->srch_len.ensure(c * 4));
-  LB_HIP(e->srch_pre.ensure((c + 1) * 4));
-  LB_HIP(e->srch_S.ensure(c * sizeof(g2j)));
+  LB_HIP(e->srch_midx.ensure(c * 4));
+  LB_HIP(e->srch_mlo.ensure((cm + 1) * 4));
+  LB_HIP(e->srch_pre.ensure((cm + 1) * 4));
+  LB_HIP(e->srch_S.ensure((cm ? cm : 1) * sizeof(g2j)));
   LB_HIP(e->srch_pk.ensure(c * sizeof(g1j)));
   LB_HIP(e->srch_verdict.ensure(c * 4));
-  LB_HIP(e->bcnt.ensure((size_t)nb * 4));
-  LB_HIP(e->bcursor.ensure((size_t)nb * 4));
-  LB_HIP(e->boff.ensure((size_t)(nb + 1) * 4));
-  LB_HIP(e->bch.ensure((size_t)(nb + 1) * 4));
-  LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
-  LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
-  LB_HIP(e->bmembers.ensure((size_t)2 * LB_MSM_W * (T ? T : 1) * 4));
-  LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
-  LB_HIP(e->bsum.ensure((size_t)nb * sizeof(g2j)));
   LB_HIP(hipMemcpyAsync(e->srch_kind.p, hk.data(), c * 4, hipMemcpyHostToDevice, s1));
   LB_HIP(hipMemcpyAsync(e->srch_key.p, hkey.data(), c * 4, hipMemcpyHostToDevice, s1));
   LB_HIP(hipMemcpyAsync(e->srch_lo.p, hlo.data(), c * 4, hipMemcpyHostToDevice, s1));
   LB_HIP(hipMemcpyAsync(e->srch_len.p, hlen.data(), c * 4, hipMemcpyHostToDevice, s1));
-  LB_HIP(hipMemcpyAsync(e->srch_pre.p, pre.data(), (c + 1) * 4, hipMemcpyHostToDevice, s1));
+  LB_HIP(hipMemcpyAsync(e->srch_midx.p, midx.data(), c * 4, hipMemcpyHostToDevice, s1));
   {
     stage_scope sc(e, ST_FALLBACK, s1);
-    // S_j by one range MSM over all nodes of this round
-    LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)nb * 4, s1));
-    LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)nb * 4, s1));
-    hipLaunchKernelGGL(k_rmsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, (uint32_t)c, e->srch_pre.as<uint32_t>(),
-                       e->srch_lo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
-                       e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
-    hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
-                       e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
-                       e->bchunk_end.as<uint32_t>());
-    hipLaunchKernelGGL(k_rmsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, (uint32_t)c,
-                       e->srch_pre.as<uint32_t>(), e->srch_lo.as<uint32_t>(), e->members.as<uint32_t>(),
-                       e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
-                       e->boff.as<uint32_t>(), e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
-    hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
-                       e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
-                       e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
-    hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
-                       e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
-    hipLaunchKernelGGL(k_msm_reduce, dim3((uint32_t)c), dim3(64), 0, s1, e->bsum.as<uint32_t>(), nb,
-                       e->srch_S.as<uint32_t>(), (uint32_t)c, 0u);
+    if (cm) {
+      LB_HIP(e->bcnt.ensure((size_t)nb * 4));
+      LB_HIP(e->bcursor.ensure((size_t)nb * 4));
+      LB_HIP(e->boff.ensure((size_t)(nb + 1) * 4));
+      LB_HIP(e->bch.ensure((size_t)(nb + 1) * 4));
+      LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
+      LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
+      LB_HIP(e->bmembers.ensure((size_t)2 * LB_MSM_W * (T ? T : 1) * 4));
+      LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
+      LB_HIP(e->bsum.ensure((size_t)nb * sizeof(g2j)));
+      LB_HIP(hipMemcpyAsync(e->srch_mlo.p, mlo.data(), cm * 4, hipMemcpyHostToDevice, s1));
+      LB_HIP(hipMemcpyAsync(e->srch_pre.p, mpre.data(), (cm + 1) * 4, hipMemcpyHostToDevice, s1));
+      // S of every kind-0/1 node by one range MSM
+      LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)nb * 4, s1));
+      LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)nb * 4, s1));
+      hipLaunchKernelGGL(k_rmsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, e->srch_pre.as<uint32_t>(),
+                         e->srch_mlo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
+                         e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
+                         e->bchunk_end.as<uint32_t>());
+      hipLaunchKernelGGL(k_rmsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, e->srch_pre.as<uint32_t>(),
+                         e->srch_mlo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
+                         e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
+      hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
+                         e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
+                         e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
+      hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
+                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
+      hipLaunchKernelGGL(k_msm_reduce, dim3(cm), dim3(64), 0, s1, e->bsum.as<uint32_t>(), nb,
+                         e->srch_S.as<uint32_t>(), cm, 0u);
+    }
     // kind-1 nodes: sum r_i PK_i over the part
     hipLaunchKernelGGL(k_range_pk, dim3(nblk((uint32_t)c)), dim3(LB_TPB), 0, s1, (uint32_t)c,
                        e->srch_kind.as<uint32_t>(), e->srch_lo.as<uint32_t>(), e->srch_len.as<uint32_t>(),
@@ -771,8 +788,10 @@ static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& 
   {
     stage_scope sc(e, ST_BISECT, s1);
     hipLaunchKernelGGL(k_search_check, dim3((uint32_t)c), dim3(64), 0, s1, (uint32_t)c, e->srch_kind.as<uint32_t>(),
-                       e->srch_key.as<uint32_t>(), e->treeP.as<uint32_t>(), 2 * mu, e->srch_pk.as<uint32_t>(),
-                       e->h_aff.as<uint32_t>(), n, e->srch_S.as<uint32_t>(), e->srch_verdict.as<int32_t>());
+                       e->srch_key.as<uint32_t>(), e->srch_midx.as<uint32_t>(), cm ? cm : 1u, e->treeP.as<uint32_t>(),
+                       2 * mu, e->srch_pk.as<uint32_t>(), e->h_aff.as<uint32_t>(), n, e->srch_S.as<uint32_t>(),
+                       e->pk_aff.as<uint32_t>(), e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                       e->set_live.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->srch_verdict.as<int32_t>());
   }
   LB_HIP(hipGetLastError());
   verdict.resize(c);
@@ -781,40 +800,45 @@ static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& 
   return LB_OK;
 }
 
-// Refines a failing node into its children (appended to `out`); a single failing set goes to
-// `bad_pos` (its position in the members array).
+// Refines a failing node into its children (appended to `out`); a failing single set goes to
+// `bad_pos` (its position in the members array).  Subtrees of the root tree descend to the
+// leaves in steps of at most 2^6 children (the first step from the root: 2^first_step); a
+// failing root with <= 512 members is checked set by set, a bigger one in 64 parts first.
 static void refine(const search_node& f, int32_t fid, uint32_t L, uint32_t nu, const std::vector<uint32_t>& goff,
-                   uint32_t tree_step, std::vector<search_node>& out, std::vector<uint32_t>& bad_pos) {
+                   const std::vector<uint32_t>& members, uint32_t tree_step, std::vector<search_node>& out,
+                   std::vector<uint32_t>& bad_pos) {
   const uint32_t mu = 1u << L;
-  if (f.kind == 0) {
-    uint32_t d = 0;
-    while ((2u << d) <= f.key) d++;  // depth of heap index key
-    if (d == L) {  // a leaf: root u's members, in up to 64 parts
-      const uint32_t u = f.key - mu, lo = goff[u], len = goff[u + 1] - goff[u];
-      if (len == 1) {
-        bad_pos.push_back(lo);
-        return;
-      }
-      const uint32_t parts = len < 64 ? len : 64, per = (len + parts - 1) / parts;
-      for (uint32_t a = 0; a < len; a += per)
-        out.push_back({1u, u, lo + a, (a + per < len ? per : len - a), fid});
-      return;
-    }
-    const uint32_t dd = d + tree_step < L ? d + tree_step : L, k = dd - d;
-    for (uint32_t v = f.key << k; v < (f.key + 1) << k; v++) {
-      const uint32_t span = L - dd, ulo = (v - (1u << dd)) << span;
-      if (ulo >= nu) break;
-      const uint32_t uhi = (((v - (1u << dd)) + 1) << span) < nu ? (((v - (1u << dd)) + 1) << span) : nu;
-      out.push_back({0u, v, goff[ulo], goff[uhi] - goff[ulo], fid});
-    }
-    return;
-  }
-  if (f.len == 1) {
+  auto singles = [&](uint32_t lo, uint32_t len) {
+    for (uint32_t q = lo; q < lo + len; q++) out.push_back({2u, members[q], q, 1u, fid});
+  };
+  auto parts = [&](uint32_t u, uint32_t lo, uint32_t len) {
+    const uint32_t per = (len + 63) / 64;
+    for (uint32_t a = 0; a < len; a += per) out.push_back({1u, u, lo + a, (a + per < len ? per : len - a), fid});
+  };
+  if (f.kind == 2) {
     bad_pos.push_back(f.lo);
     return;
   }
-  const uint32_t parts = f.len < 64 ? f.len : 64, per = (f.len + parts - 1) / parts;
-  for (uint32_t a = 0; a < f.len; a += per) out.push_back({1u, f.key, f.lo + a, (a + per < f.len ? per : f.len - a), fid});
+  if (f.kind == 1) {
+    if (f.len <= 512) singles(f.lo, f.len);
+    else parts(f.key, f.lo, f.len);
+    return;
+  }
+  uint32_t d = 0;
+  while ((2u << d) <= f.key) d++;  // depth of heap index key
+  if (d == L) {                    // a leaf: root u's members
+    const uint32_t u = f.key - mu, lo = goff[u], len = goff[u + 1] - goff[u];
+    if (len <= 512) singles(lo, len);
+    else parts(u, lo, len);
+    return;
+  }
+  const uint32_t dd = (L - d <= 6 || d + tree_step >= L) ? L : d + tree_step, k = dd - d;
+  for (uint32_t v = f.key << k; v < (f.key + 1) << k; v++) {
+    const uint32_t span = L - dd, ulo = (v - (1u << dd)) << span;
+    if (ulo >= nu) break;
+    const uint32_t uend = ((v - (1u << dd)) + 1) << span, uhi = uend < nu ? uend : nu;
+    out.push_back({0u, v, goff[ulo], goff[uhi] - goff[ulo], fid});
+  }
 }
 
 static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* out_job) {
@@ -828,35 +852,41 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
   LB_HIP(hipStreamSynchronize(e->stream));
   std::vector<search_node> failing{{0u, 1u, 0u, n, -1}};  // the root: known to fail
   std::vector<uint32_t> bad_pos;
-  const size_t kMaxNodes = 256;
+  const size_t kMaxNodes = 2048, kMaxMsm = 1024;  // per check launch (the MSM's buckets: 1024 per node)
   bool first = true;
   while (!failing.empty()) {
     std::vector<search_node> cand;
-    for (size_t k = 0; k < failing.size(); k++) refine(failing[k], (int32_t)k, L, nu, goff, first ? 8 : 6, cand, bad_pos);
+    for (size_t k = 0; k < failing.size(); k++)
+      refine(failing[k], (int32_t)k, L, nu, goff, members, first ? 10 : 6, cand, bad_pos);
     first = false;
     if (cand.empty()) break;
     std::vector<int32_t> v(cand.size()), vk;
-    for (size_t a = 0; a < cand.size(); a += kMaxNodes) {
-      const size_t c = cand.size() - a < kMaxNodes ? cand.size() - a : kMaxNodes;
+    for (size_t a = 0; a < cand.size();) {
+      // a launch takes up to kMaxNodes nodes, of which at most kMaxMsm need the range MSM
+      size_t c = 0, cm = 0;
+      while (a + c < cand.size() && c < kMaxNodes && (cand[a + c].kind == 2u || cm < kMaxMsm)) {
+        cm += cand[a + c].kind != 2u;
+        c++;
+      }
       int32_t st = check_search_nodes(e, cand, a, c, n, mu, vk);
       if (st != LB_OK) return st;
       for (size_t j = 0; j < c; j++) v[a + j] = vk[j];
+      a += c;
     }
     // fail closed: a failing node none of whose children fails (impossible for exact arithmetic)
     // condemns its whole range
-    std::vector<int> child_fail(failing.size(), 0);
+    std::vector<int> child_fail(failing.size(), 0), refined(failing.size(), 0);
     std::vector<search_node> next;
-    for (size_t j = 0; j < cand.size(); j++)
+    for (size_t j = 0; j < cand.size(); j++) {
+      refined[cand[j].parent] = 1;
       if (!v[j]) {
         child_fail[cand[j].parent]++;
         next.push_back(cand[j]);
       }
-    for (size_t k = 0; k < failing.size(); k++) {
-      bool refined = false;
-      for (const search_node& c2 : cand) refined |= c2.parent == (int32_t)k;
-      if (refined && !child_fail[k])
-        for (uint32_t q = 0; q < failing[k].len; q++) bad_pos.push_back(failing[k].lo + q);
     }
+    for (size_t k = 0; k < failing.size(); k++)
+      if (refined[k] && !child_fail[k])
+        for (uint32_t q = 0; q < failing[k].len; q++) bad_pos.push_back(failing[k].lo + q);
     failing.swap(next);
   }
   // failing sets -> their jobs (set_live makes every failing set belong to a live job)
@@ -1037,6 +1067,76 @@ extern "C" int32_t lb_aggregate_pubkeys(lb_engine* e, uint32_t n_sets, const uin
   return LB_OK;
 }
 
+extern "C" int32_t lb_aggregate_signatures(lb_engine* e, uint32_t n_groups, const uint32_t* group_offsets,
+                                           const uint8_t* sigs96, const uint32_t* sig_sizes, int32_t validate,
+                                           uint8_t* out96, int32_t* out_status) {
+  if (!e || !group_offsets || (n_groups && (!out96 || !out_status))) return LB_ERR_ARGUMENT;
+  if (group_offsets[0] != 0) return LB_ERR_ARGUMENT;
+  for (uint32_t g = 0; g < n_groups; g++)
+    if (group_offsets[g + 1] < group_offsets[g]) return LB_ERR_ARGUMENT;
+  const uint32_t n = group_offsets[n_groups];
+  if (n && !sigs96) return LB_ERR_ARGUMENT;
+  if (!n_groups) return LB_OK;
+  // chunks of <= LB_PK_CHUNK signatures, never spanning groups
+  std::vector<uint32_t> chunk_lo, group_chunk_off(n_groups + 1);
+  for (uint32_t g = 0; g < n_groups; g++) {
+    group_chunk_off[g] = (uint32_t)chunk_lo.size();
+    for (uint32_t i = group_offsets[g]; i < group_offsets[g + 1]; i += LB_PK_CHUNK) chunk_lo.push_back(i);
+  }
+  group_chunk_off[n_groups] = (uint32_t)chunk_lo.size();
+  const uint32_t nc = (uint32_t)chunk_lo.size();
+  chunk_lo.push_back(n);
+  std::lock_guard<std::mutex> lk(e->mu);
+  LB_HIP(hipSetDevice(e->device));
+  const uint32_t ns = n ? n : 1, ncs = nc ? nc : 1;
+  dbuf in, sizes, aff, aos, inf, st, clo, goff, acc, cst, out, ost;
+  hipError_t r = in.ensure((size_t)ns * 96);
+  if (r == hipSuccess) r = sizes.ensure((size_t)ns * 4);
+  if (r == hipSuccess) r = aff.ensure((size_t)ns * sizeof(g2a));
+  if (r == hipSuccess) r = aos.ensure((size_t)ns * sizeof(g2a));
+  if (r == hipSuccess) r = inf.ensure((size_t)ns * 4);
+  if (r == hipSuccess) r = st.ensure((size_t)ns * 4);
+  if (r == hipSuccess) r = clo.ensure((size_t)(nc + 1) * 4);
+  if (r == hipSuccess) r = goff.ensure((size_t)(n_groups + 1) * 4);
+  if (r == hipSuccess) r = acc.ensure((size_t)ncs * sizeof(g2j));
+  if (r == hipSuccess) r = cst.ensure((size_t)ncs * 4);
+  if (r == hipSuccess) r = out.ensure((size_t)n_groups * 96);
+  if (r == hipSuccess) r = ost.ensure((size_t)n_groups * 4);
+  hipStream_t s1 = e->stream;
+  if (r == hipSuccess && n) r = hipMemcpyAsync(in.p, sigs96, (size_t)n * 96, hipMemcpyHostToDevice, s1);
+  if (r == hipSuccess && n && sig_sizes) r = hipMemcpyAsync(sizes.p, sig_sizes, (size_t)n * 4, hipMemcpyHostToDevice, s1);
+  if (r == hipSuccess) r = hipMemcpyAsync(clo.p, chunk_lo.data(), (size_t)(nc + 1) * 4, hipMemcpyHostToDevice, s1);
+  if (r == hipSuccess)
+    r = hipMemcpyAsync(goff.p, group_chunk_off.data(), (size_t)(n_groups + 1) * 4, hipMemcpyHostToDevice, s1);
+  if (r == hipSuccess) {
+    if (n) {
+      hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, in.as<uint8_t>(),
+                         sig_sizes ? sizes.as<uint32_t>() : nullptr, aff.as<uint32_t>(), aos.as<uint4>(),
+                         inf.as<uint32_t>(), st.as<int32_t>());
+      if (validate)
+        hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, aff.as<uint32_t>(),
+                           inf.as<uint32_t>(), st.as<int32_t>());
+    }
+    if (nc)
+      hipLaunchKernelGGL(k_sig_agg_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s1, nc, clo.as<uint32_t>(),
+                         aff.as<uint32_t>(), n, inf.as<uint32_t>(), st.as<int32_t>(), acc.as<uint32_t>(),
+                         cst.as<int32_t>());
+    hipLaunchKernelGGL(k_sig_agg_groups, dim3(nblk(n_groups)), dim3(LB_TPB), 0, s1, n_groups, goff.as<uint32_t>(),
+                       acc.as<uint32_t>(), nc, cst.as<int32_t>(), out.as<uint8_t>(), ost.as<int32_t>());
+    r = hipGetLastError();
+  }
+  if (r == hipSuccess) r = hipMemcpyAsync(out96, out.p, (size_t)n_groups * 96, hipMemcpyDeviceToHost, s1);
+  if (r == hipSuccess) r = hipMemcpyAsync(out_status, ost.p, (size_t)n_groups * 4, hipMemcpyDeviceToHost, s1);
+  if (r == hipSuccess) r = hipStreamSynchronize(s1);
+  dbuf* all[] = {&in, &sizes, &aff, &aos, &inf, &st, &clo, &goff, &acc, &cst, &out, &ost};
+  for (dbuf* d : all) d->release();
+  if (r != hipSuccess) {
+    fprintf(stderr, "lodestar_bls: signature aggregation failed: %s\n", hipGetErrorString(r));
+    return LB_ERR_DEVICE;
+  }
+  return LB_OK;
+}
+
 // Generic "n items in, per-item outputs back" launcher for the small helper kernels.
 namespace {
 struct io_spec {
@@ -1074,6 +1174,32 @@ static int32_t run_simple(lb_engine* e, std::vector<io_spec> io, Launch launch) 
     return LB_ERR_DEVICE;
   }
   return LB_OK;
+}
+
+extern "C" int32_t lb_merkleize(lb_engine* e, uint32_t n_trees, const uint32_t* chunk_offsets, const uint8_t* chunks32,
+                                const uint32_t* depths, const uint64_t* mix_lengths, uint8_t* out_roots32) {
+  if (!e || !chunk_offsets || (n_trees && (!depths || !mix_lengths || !out_roots32))) return LB_ERR_ARGUMENT;
+  if (chunk_offsets[0] != 0) return LB_ERR_ARGUMENT;
+  for (uint32_t t = 0; t < n_trees; t++) {
+    const uint32_t len = chunk_offsets[t + 1] - chunk_offsets[t];
+    if (chunk_offsets[t + 1] < chunk_offsets[t] || depths[t] > 63 || (depths[t] < 32 && len > (1u << depths[t])))
+      return LB_ERR_ARGUMENT;
+  }
+  const uint32_t nc = chunk_offsets[n_trees];
+  if (nc && !chunks32) return LB_ERR_ARGUMENT;
+  if (!n_trees) return LB_OK;
+  return run_simple(e, {{chunk_offsets, (size_t)(n_trees + 1) * 4, false, nullptr},
+                        {depths, (size_t)n_trees * 4, false, nullptr},
+                        {mix_lengths, (size_t)n_trees * 8, false, nullptr},
+                        {chunks32, (size_t)nc * 32, false, nullptr},
+                        {nullptr, 64 * 32, true, nullptr},  // zero-subtree roots (device scratch)
+                        {nullptr, (size_t)n_trees * 32, true, out_roots32}},
+                    [&](std::vector<void*>& p) {
+                      hipLaunchKernelGGL(k_ssz_zero_hashes, dim3(1), dim3(64), 0, e->stream, (uint8_t*)p[4]);
+                      hipLaunchKernelGGL(k_merkleize, dim3(nblk(n_trees)), dim3(LB_TPB), 0, e->stream, n_trees,
+                                         (const uint32_t*)p[0], (const uint32_t*)p[1], (const uint64_t*)p[2],
+                                         (uint8_t*)p[3], (const uint8_t*)p[4], (uint8_t*)p[5]);
+                    });
 }
 
 extern "C" int32_t lb_g1_decompress(lb_engine* e, uint32_t n, const uint8_t* in48, uint8_t* out96,

@@ -81,6 +81,7 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 #include "lb_wave.h"
+#include "lb_ssz.h"
 
 // ---------------------------------------------------------------- block-wide batch inversion
 // Montgomery's trick across the LB_INV_TPB threads of a block: prefix and suffix products by
@@ -352,11 +353,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
 }
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
-// r * PK (Jacobian) for the per-root sums.  block of LB_INV_TPB threads (fp_inv_block)
+// r * PK (Jacobian) for the per-root sums; the affine aggregate PK itself -> pk_aff.  block of LB_INV_TPB threads (fp_inv_block)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
                                                          const uint32_t* __restrict__ chunk_acc,
                                                          const int32_t* __restrict__ chunk_status,
-                                                         const uint32_t* __restrict__ pk_off,
+                                                         uint32_t* __restrict__ pk_aff,
                                                          const uint64_t* __restrict__ scalars,
                                                          uint32_t* __restrict__ rpk,
                                                          int32_t* __restrict__ pk_status) {
@@ -398,9 +399,9 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   } else {
     rj = jac_infinity<fp>();
   }
-  (void)pk_off;
   if (!act) return;
   soa_st(rpk, n, i, rj);
+  if (ok) soa_st(pk_aff, n, i, pk);  // the unblinded aggregate, for single-set checks of the search
   pk_status[i] = st;
 }
 
@@ -676,7 +677,9 @@ __global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ 
 // contiguous range [lo_j, lo_j + len_j) of the members array (sets sorted by signing root) and
 // passes iff FE(P_j * ML(-G1, S_j)) == 1 with S_j = sum r_i sig_i over its live sets and
 //   kind 0 (a subtree of the root product tree, whole roots): P_j = treeP[v_j];
-//   kind 1 (part of one root u_j's members): P_j = ML(sum r_i PK_i, H(m_u)).
+//   kind 1 (part of one root u_j's members): P_j = ML(sum r_i PK_i, H(m_u));
+//   kind 2 (one set i): Signature.verify itself, FE(ML(PK_i, H(m_i)) ML(-G1, sig_i)) == 1,
+//          no blinding and no MSM (a set of a rejected job passes trivially).
 // By bilinearity a node's verdict is the product of its children's, so a failing node has a
 // failing child; the host descends until single sets (lb_engine.hip search_invalid).
 // Range MSM for S_j: every (set, window) digit of node j joins bucket j LB_MSM_NB + w 256 + d.
@@ -734,7 +737,8 @@ __global__ void __launch_bounds__(LB_TPB) k_rmsm_scatter(uint32_t T, uint32_t c,
     }
   }
 }
-// kind-1 nodes: Jacobian sum of r_i PK_i over the node's live members -> pk_out (SoA, stride c)
+// kind-1 nodes: Jacobian sum of r_i PK_i over the node's live members -> pk_out (SoA, stride c);
+// the range MSM (k_rmsm_*, instance m = midx of a kind-0/1 node) writes S_m to s_out (stride cm)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,
                                                        const uint32_t* __restrict__ rlo,
                                                        const uint32_t* __restrict__ rlen,
@@ -753,27 +757,46 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, c
 // One wave per node: verdict[j] = FE(P_j * ML(-G1, S_j)) == 1 (Pairing.finalverify)
 __global__ void __launch_bounds__(64) k_search_check(uint32_t c, const uint32_t* __restrict__ kind,
                                                      const uint32_t* __restrict__ key,
+                                                     const uint32_t* __restrict__ midx, uint32_t cm,
                                                      const uint32_t* __restrict__ treeP, uint32_t n2m,
                                                      const uint32_t* __restrict__ pk_out,
                                                      const uint32_t* __restrict__ h_aff, uint32_t n,
                                                      const uint32_t* __restrict__ s_out,
+                                                     const uint32_t* __restrict__ pk_aff,
+                                                     const uint32_t* __restrict__ sig_aff,
+                                                     const uint32_t* __restrict__ sig_inf,
+                                                     const uint32_t* __restrict__ set_live,
+                                                     const uint32_t* __restrict__ set_uid,
                                                      int32_t* __restrict__ verdict) {
   LBW_SHARED(S);
   __shared__ int s_inf;
   const uint32_t j = blockIdx.x;
   if (j >= c) return;
   const int lane = threadIdx.x;
+  const uint32_t kd = kind[j];
+  if (kd == 2u && !set_live[key[j]]) {  // a set of a rejected job takes no part
+    if (lane == 0) verdict[j] = 1;
+    return;
+  }
   w_init_consts(S);
-  if (kind[j] == 0u) {
+  if (kd == 0u) {
     w_load_soa12(S, LBW_A(0), treeP, n2m, key[j]);
   } else {
     if (lane == 0) {
-      const g1j pj = soa_ld<g1j>(pk_out, c, j);
+      g1j pj;
+      uint32_t u;
+      if (kd == 1u) {
+        pj = soa_ld<g1j>(pk_out, c, j);
+        u = key[j];
+      } else {
+        pj = jac_from_aff(soa_ld<g1a>(pk_aff, n, key[j]));
+        u = set_uid[key[j]];
+      }
       s_inf = jac_is_inf(pj) ? 1 : 0;
       if (!s_inf) {
         g1a pa;
         jac_to_aff(pa, pj);
-        const g2a h = soa_ld<g2a>(h_aff, n, key[j]);
+        const g2a h = soa_ld<g2a>(h_aff, n, u);
         w_st(S, LBW_PT + 0, pa.x);
         w_st(S, LBW_PT + 1, pa.y);
         w_st(S, LBW_PT + 2, h.x.c0);
@@ -791,11 +814,16 @@ __global__ void __launch_bounds__(64) k_search_check(uint32_t c, const uint32_t*
       w_miller(S, LBW_A(0));
   }
   if (lane == 0) {
-    const g2j Sj = soa_ld<g2j>(s_out, c, j);
-    s_inf = jac_is_inf(Sj) ? 1 : 0;
+    g2a a;
+    if (kd == 2u) {
+      s_inf = sig_inf[key[j]] ? 1 : 0;
+      a = soa_ld<g2a>(sig_aff, n, key[j]);
+    } else {
+      const g2j Sj = soa_ld<g2j>(s_out, cm, midx[j]);
+      s_inf = jac_is_inf(Sj) ? 1 : 0;
+      if (!s_inf) jac_to_aff(a, Sj);
+    }
     if (!s_inf) {
-      g2a a;
-      jac_to_aff(a, Sj);
       w_st(S, LBW_PT + 0, fp_load(LB_G1X));
       w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
       w_st(S, LBW_PT + 2, a.x.c0);
@@ -912,6 +940,7 @@ __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const
   LBW_SHARED(S);
   const uint32_t i = lo + blockIdx.x, span = m / lo, start = blockIdx.x * span, nu = *n_u;
   if (start >= nu) return;
+  w_init_consts(S);  // the programs' padding reads the constant zero slot
   w_load_soa12(S, LBW_A(0), treeP, 2 * m, 2 * i);
   if (start + span / 2 < nu) {
     w_load_soa12(S, LBW_A(1), treeP, 2 * m, 2 * i + 1);
@@ -1018,6 +1047,49 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_aggregate(uint32_t n, const
   g1_serialize96(ob, r, !fin || st != LB_OK);
   for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
   status[i] = st;
+}
+
+// ---------------------------------------------------------------- G2 signature aggregation
+// bls.Signature.aggregate(signatures).toBytes() as the op pools use it for block production
+// (beacon-node/src/chain/opPools/aggregatedAttestationPool.ts:321, attestationPool.ts:184,
+// syncContributionAndProofPool.ts:185): signatures decoded by k_decompress_sigs (+ k_sig_subgroup
+// when validating), summed in chunks of <= LB_PK_CHUNK per lane, then per group.
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_sig_agg_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
+                                                           const uint32_t* __restrict__ sig_aff, uint32_t n,
+                                                           const uint32_t* __restrict__ sig_inf,
+                                                           const int32_t* __restrict__ sig_status,
+                                                           uint32_t* __restrict__ chunk_acc,
+                                                           int32_t* __restrict__ chunk_status) {
+  const uint32_t c = lb_tid();
+  if (c >= nc) return;
+  int st = LB_OK;
+  g2j acc = jac_infinity<fp2>();
+  for (uint32_t i = chunk_lo[c]; i < chunk_lo[c + 1] && st == LB_OK; i++) {
+    st = sig_status[i];
+    if (st == LB_OK && !sig_inf[i]) acc = jac_add_aff_i<fp2, true>(acc, soa_ld<g2a>(sig_aff, n, i));
+  }
+  soa_st(chunk_acc, nc, c, acc);
+  chunk_status[c] = st;
+}
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_agg_groups(uint32_t ng, const uint32_t* __restrict__ group_chunk_off,
+                                                           const uint32_t* __restrict__ chunk_acc, uint32_t nc,
+                                                           const int32_t* __restrict__ chunk_status,
+                                                           uint8_t* __restrict__ out96, int32_t* __restrict__ status) {
+  const uint32_t g = lb_tid();
+  if (g >= ng) return;
+  const uint32_t c0 = group_chunk_off[g], c1 = group_chunk_off[g + 1];
+  int st = c0 == c1 ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+  g2j acc = jac_infinity<fp2>();
+  for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
+    st = chunk_status[c];
+    if (st == LB_OK) acc = jac_add(acc, soa_ld<g2j>(chunk_acc, nc, c));
+  }
+  g2a a;
+  const bool fin = st == LB_OK && jac_to_aff(a, acc);
+  uint8_t ob[96];
+  g2_compress96(ob, a, !fin);
+  for (int k = 0; k < 96; k++) out96[(size_t)96 * g + k] = ob[k];
+  status[g] = st;
 }
 
 // ---------------------------------------------------------------- G1 decompression

@@ -21,10 +21,10 @@ class BlsError(Exception):
     """A job rejected with a blst-style error (message = the reference's error string,
     e.g. "BLST_INVALID_SIZE", multithread.test.ts:97)."""
 
-    def __init__(self, code: int, name: Optional[str] = None):
+    def __init__(self, code: int, message: Optional[str] = None):
         self.code = int(code)
-        self.name = name if name is not None else N.error_name(code)
-        super().__init__(self.name)
+        self.name = N.error_name(code)
+        super().__init__(message if message is not None else self.name)
 
 
 @dataclass
@@ -253,6 +253,33 @@ class Engine:
         st = np.zeros(max(n, 1), dtype=np.int32)
         _check(self.lib.lb_aggregate_pubkeys(self.h, n, _p(offa, ctypes.c_uint32), _p(pka, ctypes.c_uint8),
                                              _p(out, ctypes.c_uint8), _p(st, ctypes.c_int32)))
+        ob = out.tobytes()
+        return [ob[96 * i: 96 * i + 96] for i in range(n)], [int(x) for x in st[:n]]
+
+    def aggregate_signatures(self, groups: Sequence[Sequence[bytes]], validate: bool = True
+                             ) -> Tuple[List[bytes], List[int]]:
+        """bls.Signature.aggregate per group (lb_aggregate_signatures): 96-byte compressed sums
+        and per-group status (0 = ok, else the blst error code)."""
+        off = [0]
+        flat, sizes, odd = [], [], False
+        for g in groups:
+            for sg in g:
+                sg = bytes(sg)
+                sizes.append(len(sg))
+                if len(sg) != 96:
+                    odd = True
+                    sg = (sg + bytes(96))[:96]
+                flat.append(sg)
+            off.append(off[-1] + len(g))
+        n = len(groups)
+        offa = np.asarray(off, dtype=np.uint32)
+        buf = np.frombuffer(b"".join(flat), dtype=np.uint8).copy() if flat else np.zeros(1, np.uint8)
+        sz = np.asarray(sizes, dtype=np.uint32) if odd else None
+        out = np.zeros(max(n, 1) * 96, dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        _check(self.lib.lb_aggregate_signatures(self.h, n, _p(offa, ctypes.c_uint32), _p(buf, ctypes.c_uint8),
+                                                _p(sz, ctypes.c_uint32), 1 if validate else 0,
+                                                _p(out, ctypes.c_uint8), _p(st, ctypes.c_int32)))
         ob = out.tobytes()
         return [ob[96 * i: 96 * i + 96] for i in range(n)], [int(x) for x in st[:n]]
 

@@ -36,9 +36,17 @@ export declare class BlsGpuVerifier implements IBlsVerifier {
   /** 48- or 96-byte keys -> handles carrying their table index (validate: keyValidate checks) */
   registerPubkeys(keys: Uint8Array[], validate?: boolean): GpuPublicKey[];
   verifySignatureSets(sets: ISignatureSet[], opts?: VerifySignatureOpts): Promise<boolean>;
+  /** state-transition verifySignatureSet: synchronous, throws the blst error on malformed input */
+  verifySignatureSet(set: ISignatureSet): boolean;
+  /** bls.Signature.aggregate(signatures).toBytes() (op pools), 96-byte compressed */
+  aggregateSignatures(signatures: Uint8Array[], validate?: boolean): Uint8Array;
   close(): Promise<void>;
   readonly stats: {batches: number; jobs: number; sets: number; jobsInvalid: number; jobsError: number};
 }
+
+/** light-client isValidBlsAggregate (validation.ts:154-184) with its stage-prefixed errors */
+export declare function isValidBlsAggregate(verifier: BlsGpuVerifier, publicKeys: PublicKeyLike[],
+                                            message: Uint8Array, signature: Uint8Array): boolean;
 
 export declare function chunkifyMaximizeChunkSize<T>(arr: T[], minPerChunk: number): T[][];
 export declare const MAX_SIGNATURE_SETS_PER_JOB: number;

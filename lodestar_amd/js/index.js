@@ -185,6 +185,37 @@ class BlsGpuVerifier {
   }
 
   /**
+   * state-transition verifySignatureSet (src/util/signatureSets.ts:24-38): synchronous; `single`
+   * -> Signature.verify, `aggregate` -> Signature.verifyAggregate; throws the blst error on
+   * malformed input.
+   * @returns {boolean}
+   */
+  verifySignatureSet(set) {
+    validateSets([set]);
+    return codeToResult(addon.verifyJobsSync(this.engines[0], ...packJobs([[set]]))[0]);
+  }
+
+  /**
+   * bls.Signature.aggregate(signatures).toBytes() for block production (chain/opPools/*).
+   * @param {Uint8Array[]} signatures 96-byte compressed
+   * @returns {Uint8Array} 96-byte compressed aggregate
+   */
+  aggregateSignatures(signatures, validate) {
+    const flat = new Uint8Array(96 * signatures.length);
+    const sizes = new Uint32Array(signatures.length);
+    let odd = false;
+    signatures.forEach((sg, i) => {
+      sizes[i] = sg.length;
+      if (sg.length === 96) flat.set(sg, 96 * i);
+      else odd = true;
+    });
+    const r = addon.aggregateSignatures(this.engines[0], Uint32Array.from([0, signatures.length]), flat,
+      odd ? sizes : null, validate === undefined ? true : Boolean(validate));
+    if (r.status[0] !== 0) throw Error(addon.errorName(r.status[0]));
+    return r.out;
+  }
+
+  /**
    * @param {Array} sets ISignatureSet[]
    * @param {{batchable?: boolean, verifyOnMainThread?: boolean}} [opts]
    * @returns {Promise<boolean>}
@@ -285,8 +316,25 @@ class BlsGpuVerifier {
   }
 }
 
+/**
+ * light-client/src/validation.ts:154-184 isValidBlsAggregate: aggregate the participants' keys,
+ * decode the signature, verify -- with the reference's stage-prefixed error messages.
+ */
+function isValidBlsAggregate(verifier, publicKeys, message, signature) {
+  try {
+    return verifier.verifySignatureSet({type: SignatureSetType.aggregate, pubkeys: publicKeys, signingRoot: message,
+                                        signature});
+  } catch (e) {
+    const stage = e.message === "EMPTY_AGGREGATE_ARRAY" ? "Error aggregating pubkeys"
+      : e.message === "BLST_PK_IS_INFINITY" ? "Error verifying signature" : "Error deserializing signature";
+    e.message = `${stage}: ${e.message}`;
+    throw e;
+  }
+}
+
 module.exports = {
   BlsGpuVerifier,
+  isValidBlsAggregate,
   GpuPublicKey,
   QueueError,
   SignatureSetType,

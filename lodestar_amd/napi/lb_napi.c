@@ -30,6 +30,8 @@
  *     -> {first: number, status: Int32Array}   (lb_pubkey_table_append: the index2pubkey cache)
  *   tableSize(engine) -> number
  *   g1Decompress(engine, keys48: Uint8Array) -> {out: Uint8Array, status: Int32Array}
+ *   aggregateSignatures(engine, groupOffsets: Uint32Array, sigs: Uint8Array, sigSizes?, validate?)
+ *     -> {out: Uint8Array (96 B per group), status: Int32Array}
  *   aggregatePubkeys(engine, setPkOffsets: Uint32Array, pubkeys: Uint8Array)
  *     -> {out: Uint8Array, status: Int32Array}
  *   errorName(code: number) -> string
@@ -439,6 +441,56 @@ static napi_value register_pubkeys(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+/* aggregateSignatures(engine, groupOffsets: Uint32Array, sigs: Uint8Array (96 B each),
+ *                     sigSizes: Uint32Array | null, validate: boolean)
+ *   -> {out: Uint8Array (96 B per group), status: Int32Array}   (lb_aggregate_signatures) */
+static napi_value aggregate_signatures(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview off, sg, sz;
+  memset(&sz, 0, sizeof(sz));
+  bool validate = true;
+  if (argc < 3 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &off) || !off.present || off.type != napi_uint32_array || off.n < 1 ||
+      !get_view(env, argv[2], &sg) || (sg.present && sg.type != napi_uint8_array) ||
+      (argc >= 4 && !get_view(env, argv[3], &sz)) || (sz.present && sz.type != napi_uint32_array)) {
+    napi_throw_type_error(env, NULL, "aggregateSignatures(engine, groupOffsets, sigs, sigSizes?, validate?)");
+    return NULL;
+  }
+  if (argc >= 5) napi_get_value_bool(env, argv[4], &validate);
+  const uint32_t* o = (const uint32_t*)off.data;
+  const uint32_t ng = (uint32_t)(off.n - 1);
+  if (o[0] != 0) {
+    napi_throw_type_error(env, NULL, "groupOffsets[0] must be 0");
+    return NULL;
+  }
+  for (uint32_t g = 0; g < ng; g++)
+    if (o[g + 1] < o[g]) {
+      napi_throw_type_error(env, NULL, "groupOffsets must be non-decreasing");
+      return NULL;
+    }
+  const size_t n = o[ng];
+  if (n * 96 > (sg.present ? sg.n : 0) || (sz.present && sz.n < n)) {
+    napi_throw_type_error(env, NULL, "sigs / sigSizes shorter than groupOffsets[nGroups] signatures");
+    return NULL;
+  }
+  napi_value ab_o, ab_s, out_o, out_s, obj;
+  void *po, *ps;
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)ng * 96, &po, &ab_o));
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)ng * 4, &ps, &ab_s));
+  int32_t st = lb_aggregate_signatures(b->e, ng, o, (const uint8_t*)sg.data, sz.present ? (const uint32_t*)sz.data : NULL,
+                                       validate ? 1 : 0, (uint8_t*)po, (int32_t*)ps);
+  if (st != LB_OK) return throw_code(env, st);
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, (size_t)ng * 96, ab_o, 0, &out_o));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, ng, ab_s, 0, &out_s));
+  NAPI_CALL(env, napi_create_object(env, &obj));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "out", out_o));
+  NAPI_CALL(env, napi_set_named_property(env, obj, "status", out_s));
+  return obj;
+}
+
 /* g1Decompress(engine, keys48: Uint8Array) -> {out: Uint8Array (96 B per key), status: Int32Array} */
 static napi_value g1_decompress(napi_env env, napi_callback_info info) {
   size_t argc = 2;
@@ -496,6 +548,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"registerPubkeys", NULL, register_pubkeys, NULL, NULL, NULL, napi_default, NULL},
       {"tableSize", NULL, table_size, NULL, NULL, NULL, napi_default, NULL},
       {"g1Decompress", NULL, g1_decompress, NULL, NULL, NULL, napi_default, NULL},
+      {"aggregateSignatures", NULL, aggregate_signatures, NULL, NULL, NULL, napi_default, NULL},
       {"errorName", NULL, error_name, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);

@@ -223,6 +223,20 @@ class BlsGpuVerifier:
             for e in self.engines:
                 e.close()
 
+    # ---------------------------------------------------------------- direct (non-pool) callers
+    def verify_signature_set(self, s: ISignatureSet) -> bool:
+        """state-transition verifySignatureSet (src/util/signatureSets.ts:24-38): synchronous, the
+        signature subgroup-checked, `single` -> Signature.verify, `aggregate` ->
+        Signature.verifyAggregate (fastAggregateVerify).  Raises BlsError on malformed input."""
+        return _result(self.engine.verify_jobs([[_to_input(s)]])[0])
+
+    def aggregate_signatures(self, signatures: Sequence[bytes], validate: bool = True) -> bytes:
+        """bls.Signature.aggregate(sigs).toBytes() (chain/opPools/*: block production), on the GPU."""
+        out, st = self.engine.aggregate_signatures([list(signatures)], validate)
+        if st[0]:
+            raise BlsError(st[0])
+        return out[0]
+
     def register_pubkeys(self, pks: Sequence[bytes], validate: bool = False) -> List[PublicKey]:
         """Load keys (48-byte compressed or 96-byte uncompressed) into the GPU-resident table once,
         like the epoch cache's index2pubkey (pubkeyCache.ts:56-77); returned PublicKeys carry their
@@ -310,3 +324,20 @@ def _set_res(f: asyncio.Future, v):
 def _set_exc(f: asyncio.Future, e):
     if not f.done():
         f.set_exception(e)
+
+
+_PK_STAGE = {"EMPTY_AGGREGATE_ARRAY"}
+_VERIFY_STAGE = {"BLST_PK_IS_INFINITY"}
+
+
+def is_valid_bls_aggregate(verifier: BlsGpuVerifier, public_keys: Sequence[PublicKey], message: bytes,
+                           signature: bytes) -> bool:
+    """light-client/src/validation.ts:154-184 isValidBlsAggregate: PublicKey.aggregate, then
+    Signature.fromBytes(.., true), then verify, with the reference's stage-prefixed error messages.
+    Used for sync-committee aggregates of light-client updates."""
+    try:
+        return verifier.verify_signature_set(AggregatedSignatureSet(list(public_keys), bytes(message), bytes(signature)))
+    except BlsError as e:
+        stage = ("Error aggregating pubkeys" if e.name in _PK_STAGE else
+                 "Error verifying signature" if e.name in _VERIFY_STAGE else "Error deserializing signature")
+        raise BlsError(e.code, f"{stage}: {e.name}") from None

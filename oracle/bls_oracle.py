@@ -337,6 +337,10 @@ def g2_neg(pt):
     return None if pt is None else (pt[0], f2_neg(pt[1]))
 
 
+def g2_neg(pt):
+    return None if pt is None else (pt[0], f2_neg(pt[1]))
+
+
 def g2_mul(pt, k: int):
     if k < 0:
         return g2_mul(g2_neg(pt), -k)

@@ -173,10 +173,42 @@ def aggregates():
                     "status": "BLST_SUCCESS"})
     out.append({"pubkeys": [], "expected96": h(bytes([0x40]) + bytes(95)), "status": "EMPTY_AGGREGATE_ARRAY"})
     comp = [{"in48": h(o.g1_compress(p)), "out96": h(o.g1_serialize(p))} for p in pts]
-    return {"aggregate": out, "g1_decompress": comp}
+    return {"aggregate": out, "g1_decompress": comp, "signature_aggregate": signature_aggregates()}
+
+
+def signature_aggregates():
+    """bls.Signature.aggregate over decoded signatures (the opPools' aggregation,
+    chain/opPools/aggregatedAttestationPool.ts:321): ZCash compressed G2 sum, infinity = 0xc0.
+    Decoding follows Signature.fromBytes(.., validate); the first bad signature's error rejects
+    the group, an empty group rejects with EMPTY_AGGREGATE_ARRAY."""
+    keys = [o.interop_secret_key(i) for i in range(4)]
+    msgs = [bytes([0x20 + i]) * 32 for i in range(4)]
+    pts = [o.sign(k, m) for k, m in zip(keys, msgs)]
+    comp = [o.g2_compress(p) for p in pts]
+    neg0 = o.g2_compress(o.g2_neg(pts[0]))
+    inf = bytes([0xC0]) + bytes(95)
+    groups = [[0], [0, 1], [0, 1, 2, 3], [0, 0], [0, "n0"], ["inf", 1], [2, "inf", 3]]
+    out = []
+    for g in groups:
+        sigs = [neg0 if x == "n0" else inf if x == "inf" else comp[x] for x in g]
+        acc = None
+        for b in sigs:
+            acc = o.g2_add(acc, o.signature_from_bytes(b, True))
+        out.append({"signatures": [h(b) for b in sigs], "expected96": h(o.g2_compress(acc)), "status": "BLST_SUCCESS"})
+    bad = bytearray(comp[1])
+    bad[0] &= 0x7F
+    out.append({"signatures": [h(comp[0]), h(bytes(bad))], "expected96": None, "status": "BLST_BAD_ENCODING"})
+    out.append({"signatures": [h(comp[0]), h(g2_point_off_subgroup())], "expected96": None,
+                "status": "BLST_POINT_NOT_IN_GROUP"})
+    out.append({"signatures": [], "expected96": None, "status": "EMPTY_AGGREGATE_ARRAY"})
+    return out
 
 
 if __name__ == "__main__":
+    if "--aggregates-only" in sys.argv:
+        with open(os.path.join(OUT, "aggregates.json"), "w") as f:
+            json.dump(aggregates(), f, indent=1)
+        sys.exit(0)
     print("kats", flush=True)
     with open(os.path.join(OUT, "reference_kats.json"), "w") as f:
         json.dump(kats(), f, indent=1)

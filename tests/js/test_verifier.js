@@ -117,6 +117,22 @@ async function gpuTests() {
   m.addon.destroyEngine(eng);
   assert.deepStrictEqual(Array.from(await inflight), [1]);
   assert.throws(() => m.addon.verifyJobs(eng, ...single), /engine destroyed/);
+  // direct callers: verifySignatureSet (state transition), isValidBlsAggregate (light client),
+  // aggregateSignatures (op pools)
+  const byName = Object.fromEntries(cases.map((c) => [c.name, c]));
+  assert.strictEqual(pool.verifySignatureSet(setsFromCase(byName.single_valid_0)[0]), true);
+  assert.strictEqual(pool.verifySignatureSet(setsFromCase(byName.aggregate_valid)[0]), true);
+  assert.strictEqual(pool.verifySignatureSet(setsFromCase(byName.wrong_message)[0]), false);
+  assert.throws(() => pool.verifySignatureSet(setsFromCase(byName.invalid_size_32_zero)[0]), /BLST_INVALID_SIZE/);
+  const av = setsFromCase(byName.aggregate_valid)[0];
+  assert.strictEqual(m.isValidBlsAggregate(pool, av.pubkeys, av.signingRoot, av.signature), true);
+  assert.throws(() => m.isValidBlsAggregate(pool, [], av.signingRoot, av.signature),
+    /^Error: Error aggregating pubkeys: EMPTY_AGGREGATE_ARRAY$/);
+  for (const g of golden("aggregates.json").signature_aggregate) {
+    const sigs = g.signatures.map(hex);
+    if (g.status === "BLST_SUCCESS") assert.strictEqual(Buffer.from(pool.aggregateSignatures(sigs)).toString("hex"), g.expected96);
+    else assert.throws(() => pool.aggregateSignatures(sigs), new RegExp(g.status));
+  }
   // close(): queued jobs abort
   const pending = outcome(pool.verifySignatureSets(k4, {batchable: true}));
   await pool.close();

@@ -494,3 +494,70 @@ def test_indexed_null_indices_only_without_keys(engine):
     st = lib.lb_verify_jobs_indexed(engine.h, 1, p32(job_off), p32(pk0), None, p8(msgs), p8(sigs), None, None,
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
     assert st == N.LB_OK and out[0] == -N.LB_EMPTY_AGGREGATE_ARRAY
+
+
+def test_search_large_roots_parts_then_sets(engine):
+    """Roots with > 512 members are searched in 64 parts first (one Miller loop per part of the
+    blinded sum), then set by set; every planted wrong-message set is found."""
+    bad = {5, 777, 1400}
+    jobs = make_shared_batch(engine, 1500, 2, seed=31, invalid=bad)
+    codes, prof = _verify_profiled(engine, jobs)
+    assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
+    assert prof["search_check"] > 0.0
+
+
+def test_search_c3_invalid_two_slots(engine):
+    """c3 with one wrong-message attestation per slot (2 slots, 38 912 sets): the search over
+    root subtrees, roots and single sets finds exactly the planted jobs."""
+    from lodestar_amd import workloads as W
+    wl = W.make(engine, "c3_invalid", slots=2)
+    b = engine.upload(W.indexed_for(engine, wl))
+    try:
+        got = np.asarray(b.verify())
+    finally:
+        b.free()
+    assert np.array_equal(got, wl.expected)
+    assert (wl.expected == 0).sum() == 2
+
+
+def test_aggregate_signatures_golden(engine):
+    """bls.Signature.aggregate on the GPU against the oracle's golden
+    groups: sums (with duplicates, cancellation to infinity, infinity members), the first bad
+    signature's error, EMPTY_AGGREGATE_ARRAY."""
+    from lodestar_amd import _native as N
+    g = load_json("aggregates.json")["signature_aggregate"]
+    out, st = engine.aggregate_signatures([[bytes.fromhex(x) for x in c["signatures"]] for c in g], validate=True)
+    for c, o_, s in zip(g, out, st):
+        assert N.error_name(s) == c["status"], c
+        if c["expected96"] is not None:
+            assert o_.hex() == c["expected96"]
+
+
+def test_direct_verify_callers(engine):
+    """state-transition verifySignatureSet and the light client's isValidBlsAggregate (SURVEY.md
+    §8(f) row 3) on the golden sets, including the reference's stage-prefixed errors."""
+    from lodestar_amd import verifier as V
+    cases = {c["name"]: c for c in load_json("jobs.json")["cases"]}
+    pool = V.BlsGpuVerifier(engine=engine)
+    try:
+        def as_set(c, agg):
+            s = c["sets"][0]
+            pks = [V.PublicKey(bytes.fromhex(p)) for p in s["pubkeys"]]
+            root, sig = bytes.fromhex(s["signing_root"]), bytes.fromhex(s["signature"])
+            return V.AggregatedSignatureSet(pks, root, sig) if agg else V.SingleSignatureSet(pks[0], root, sig)
+        assert pool.verify_signature_set(as_set(cases["single_valid_0"], False)) is True
+        assert pool.verify_signature_set(as_set(cases["aggregate_valid"], True)) is True
+        assert pool.verify_signature_set(as_set(cases["wrong_message"], False)) is False
+        with pytest.raises(BlsError, match="BLST_INVALID_SIZE"):
+            pool.verify_signature_set(as_set(cases["invalid_size_32_zero"], False))
+        agg = as_set(cases["aggregate_valid"], True)
+        assert V.is_valid_bls_aggregate(pool, agg.pubkeys, agg.signing_root, agg.signature) is True
+        with pytest.raises(BlsError, match="^Error aggregating pubkeys: EMPTY_AGGREGATE_ARRAY$"):
+            V.is_valid_bls_aggregate(pool, [], agg.signing_root, agg.signature)
+        bad = as_set(cases["not_in_group"], False)
+        with pytest.raises(BlsError, match="^Error deserializing signature: BLST_POINT_NOT_IN_GROUP$"):
+            V.is_valid_bls_aggregate(pool, [bad.pubkey], bad.signing_root, bad.signature)
+        sigs = [bytes.fromhex(x) for x in load_json("aggregates.json")["signature_aggregate"][2]["signatures"]]
+        assert pool.aggregate_signatures(sigs).hex() == load_json("aggregates.json")["signature_aggregate"][2]["expected96"]
+    finally:
+        asyncio.run(pool.close())
