@@ -12,6 +12,9 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -109,9 +112,9 @@ struct lb_engine {
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum;
   // invalid-set search (search_invalid): node descriptors and per-node results
-  dbuf srch_kind, srch_key, srch_lo, srch_len, srch_pre, srch_S, srch_pk, srch_verdict;
+  dbuf sx[32];   // search round buffers (search_invalid: SX_*)
   dbuf pk_aff;  // affine aggregate pubkey per set (single-set checks of the search)
-  dbuf srch_midx, srch_mlo;
+  dbuf y_root;  // FE value of the root check (the search starts from it)
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -122,6 +125,7 @@ struct lb_engine {
   hipEvent_t ev0[kStages] = {}, ev1[kStages] = {};
   bool used[kStages] = {};
   float last_ms[kStages] = {};
+  float acc_ms[kStages] = {};  // stages run once per search round: summed over the rounds
   // pinned host word for the distinct-root count read back after grouping: the per-root kernels
   // are launched over that count, not over the set count (their scratch is sized per dispatch)
   uint32_t* h_nu = nullptr;
@@ -226,7 +230,14 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   e->device = device;
   while (getrandom(&e->msg_key, 8, 0) != 8) {
   }
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+  // s1 carries the latency-bound chain (grouping, per-root hashing and Miller loops, the root
+  // check, the invalid-set search); LB_S1_PRIORITY=1 gives it the device's highest stream priority
+  // so its few-wave kernels are dispatched ahead of the other batches' wide ones
+  int prio_least = 0, prio_greatest = 0;
+  hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+  const char* pv = getenv("LB_S1_PRIORITY");
+  const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
+  if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
@@ -258,10 +269,9 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
-                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->srch_kind, &e->srch_key,
-                  &e->srch_lo, &e->srch_len, &e->srch_pre, &e->srch_S, &e->srch_pk, &e->srch_verdict,
-                  &e->pk_aff, &e->srch_midx, &e->srch_mlo};
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root};
   for (dbuf* b : bufs) b->release();
+  for (dbuf& b : e->sx) b.release();
   for (int i = 0; i < kStages; i++) {
     if (e->ev0[i]) hipEventDestroy(e->ev0[i]);
     if (e->ev1[i]) hipEventDestroy(e->ev1[i]);
@@ -547,7 +557,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   const uint32_t nc = b->n_chunks;
   LB_HIP(e->chunk_acc.ensure((size_t)(nc ? nc : 1) * sizeof(g1j)));
   LB_HIP(e->chunk_status.ensure((size_t)(nc ? nc : 1) * 4));
-  for (int k = 0; k < kStages; k++) e->used[k] = false;
+  for (int k = 0; k < kStages; k++) {
+    e->used[k] = false;
+    e->acc_ms[k] = 0.f;
+  }
   hipStream_t s1 = e->stream, s2 = e->stream2;
   if (e->profiling) {
     hipEventRecord(e->ev0[ST_TOTAL], s1);
@@ -644,7 +657,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(LB_MSM_NB)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
                          e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB);
-      hipLaunchKernelGGL(k_msm_reduce, dim3(1), dim3(64), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
+      hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(1), dim3(16 * LB_MSM_W), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
                          e->treeS.as<uint32_t>(), 2 * mj, 1u);
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
@@ -695,55 +708,163 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
 // After a failing root check: find the failing SETS (a job fails iff one of its live sets does;
 // per-job verdicts then equal the reference's per-job re-verification, worker.ts:76-98, up to
 // the 2^-64 soundness of the blinding).  Nodes are ranges of the members array (sets sorted by
-// signing root, lb_kernels.h k_search_check): first subtrees of the root product tree (P from
-// the tree, no new Miller loop), then parts of one failing root (P = one Miller loop of the
-// part's sum r_i PK_i with that root's H(m)), each checked with one final exponentiation, with a
-// fan-out of up to 256 (first level) / 64 nodes, so a single invalid set among ~10^5 is found in
-// about four levels of wave-parallel checks.  Costs scale with the failing ranges, not the batch:
-// the range MSMs touch each member once per level it is under a failing node.
+// signing root): subtrees of the root product tree (P from the tree), then parts of one root
+// (P = one Miller loop of the part's sum r_i PK_i with that root's H(m)).  A failing node
+// carries its FE value y.  Two moves (lb_kernels.h k_search_check / k_search_test):
+//   direct:   each child c of a node gets its own check, y_c = FE(X_c);
+//   weighted: one FE of prod_c X_c^(c+1) names the failing child when exactly one fails.
+// A failing node descends by a weighted test (one wave for up to 64 children); if the test finds
+// two or more failing children, they are checked directly, each failing child in the same round
+// getting a weighted test over its own children.  The root starts with direct checks, so one
+// round settles two levels.  Costs: a few waves and range MSMs over the failing ranges per
+// round; about four rounds for a batch of ~10^5 sets with a handful of invalid ones.
 namespace {
-struct search_node {
-  uint32_t kind, key, lo, len;  // kind 0: key = heap index in the root tree; 1: key = root id;
-                                // 2: key = set index (one set, lo = its members position)
-  int32_t parent;               // index of the failing node this one refines (-1: the root)
+struct snode {
+  uint32_t kind;  // 0: node `key` of the root product tree at depth d (d == L: the leaf of root key - mu);
+                  // 1: part of root `key`; 2: the single set `key`, checked unblinded
+  uint32_t key, lo, len, d;
+};
+struct fnode {
+  snode s;
+  bool multi;  // the last weighted test over its children found no single failing child
+  std::vector<uint32_t> y;  // FE value (144 words, the k_root_check / k_search_check layout)
+};
+struct search_ctx {
+  uint32_t n, nu, mu, L;
+  std::vector<uint32_t> goff, members;
+};
+enum {
+  SX_KIND, SX_KEY, SX_LO, SX_LEN, SX_MIDX, SX_VERDICT, SX_Y, SX_PK,  // direct checks
+  SX_MPRE, SX_MLO, SX_MMODE, SX_MWA, SX_MWB, SX_S,                     // MSM instances
+  SX_TMODE, SX_TF, SX_TV0, SX_TU, SX_TMIDX, SX_TYIDX, SX_TLO, SX_TLEN, SX_TPER, SX_TOUT, SX_TPK, SX_YUP,
+  SX_ML, SX_COUNT
+};
+static_assert(SX_COUNT <= 32, "lb_engine::sx");
+struct test_job {
+  snode node;
+  std::vector<snode> ch;
+  bool fresh;    // y from the host (a node failing in an earlier round); else from direct check `d`
+  uint32_t src;  // fresh: index into F; else index into D
 };
 }  // namespace
 
-static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& nd, size_t a, size_t c, uint32_t n,
-                                  uint32_t mu, std::vector<int32_t>& verdict) {
+// children of a failing node: direct checks fan out to depth max(d + 1, min(d + 7, L - 6)) so a
+// weighted test of each failing child can reach the leaves; weighted tests to depth d + 6 (<= 64
+// children); a root's members in <= 64 parts
+static void search_children(const search_ctx& x, const snode& a, bool direct, std::vector<snode>& out) {
+  out.clear();
+  if (a.kind == 2u || a.len <= 1) return;
+  auto parts = [&](uint32_t u, uint32_t lo, uint32_t len) {
+    const uint32_t per = (len + 63) / 64;
+    for (uint32_t q = 0; q < len; q += per) {
+      const uint32_t l = per < len - q ? per : len - q;
+      if (l == 1 && direct) out.push_back({2u, x.members[lo + q], lo + q, 1u, 0u});
+      else out.push_back({1u, u, lo + q, l, 0u});
+    }
+  };
+  if (a.kind == 1u) return parts(a.key, a.lo, a.len);
+  if (a.d == x.L) return parts(a.key - x.mu, a.lo, a.len);
+  const int d = (int)a.d, L = (int)x.L;
+  int dd = direct ? std::max(d + 1, std::min(d + 7, L - 6)) : d + 6;
+  if (dd > L) dd = L;
+  const uint32_t k = (uint32_t)(dd - d), span = (uint32_t)(L - dd);
+  for (uint32_t v = a.key << k; v < (a.key + 1) << k; v++) {
+    const uint32_t ulo = (v - (1u << dd)) << span;
+    if (ulo >= x.nu) break;
+    const uint32_t uhi = std::min(x.nu, ulo + (1u << span));
+    out.push_back({0u, v, x.goff[ulo], x.goff[uhi] - x.goff[ulo], (uint32_t)dd});
+  }
+}
+
+template <class T>
+static hipError_t sx_up(lb_engine* e, int k, const std::vector<T>& v, hipStream_t s) {
+  hipError_t r = e->sx[k].ensure((v.empty() ? 1 : v.size()) * sizeof(T));
+  if (r == hipSuccess && !v.empty()) r = hipMemcpyAsync(e->sx[k].p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  return r;
+}
+
+// One launch set: direct checks D, then weighted tests (fresh ones first).  Outputs the direct
+// verdicts and FE values (144 words each) and each test's matched child (1-based, 0: none).
+static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector<fnode>& F, const std::vector<snode>& D,
+                            const std::vector<test_job>& tests, uint32_t n_fresh, std::vector<int32_t>& verdict,
+                            std::vector<uint32_t>& ydir, std::vector<int32_t>& tout) {
   hipStream_t s1 = e->stream;
-  // node arrays; the range MSM runs over the kind-0/1 nodes only (midx = their MSM instance)
-  std::vector<uint32_t> hk(c), hkey(c), hlo(c), hlen(c), midx(c), mlo, mpre{0};
-  for (size_t j = 0; j < c; j++) {
-    const search_node& x = nd[a + j];
-    hk[j] = x.kind;
-    hkey[j] = x.key;
-    hlo[j] = x.lo;
-    hlen[j] = x.len;
-    midx[j] = 0;
-    if (x.kind != 2u) {
-      midx[j] = (uint32_t)mlo.size();
-      mlo.push_back(x.lo);
-      mpre.push_back(mpre.back() + x.len);
+  const uint32_t c = (uint32_t)D.size(), nt = (uint32_t)tests.size(), n = x.n;
+  std::vector<uint32_t> dk(c), dkey(c), dlo(c), dlen(c), dm(c, 0);
+  std::vector<uint32_t> mlo, mpre{0}, mmode, mwa, mwb;
+  auto msm = [&](uint32_t lo, uint32_t len, uint32_t mode, uint32_t wa, uint32_t wb) {
+    mlo.push_back(lo);
+    mpre.push_back(mpre.back() + len);
+    mmode.push_back(mode);
+    mwa.push_back(wa);
+    mwb.push_back(wb);
+    return (uint32_t)mlo.size() - 1;
+  };
+  for (uint32_t j = 0; j < c; j++) {
+    dk[j] = D[j].kind;
+    dkey[j] = D[j].key;
+    dlo[j] = D[j].lo;
+    dlen[j] = D[j].len;
+    if (D[j].kind != 2u) dm[j] = msm(D[j].lo, D[j].len, 0u, 1u, 0u);
+  }
+  std::vector<uint32_t> tmode(nt), tf(nt), tv0(nt), tu(nt), tm(nt), tyi(nt), tlo(nt), tlen(nt), tper(nt);
+  std::vector<uint32_t> yup((size_t)144 * (n_fresh ? n_fresh : 1));
+  for (uint32_t t = 0; t < nt; t++) {
+    const test_job& T = tests[t];
+    const snode& a = T.node;
+    const snode& c0 = T.ch[0];
+    tf[t] = (uint32_t)T.ch.size();
+    tlo[t] = a.lo;
+    tlen[t] = a.len;
+    tyi[t] = T.src;
+    if (c0.kind == 0u) {  // subtrees of 2^span roots from root ulo0
+      const uint32_t span = x.L - c0.d, ulo0 = (c0.key - (1u << c0.d)) << span;
+      tmode[t] = 1u;
+      tv0[t] = c0.key;
+      tm[t] = msm(a.lo, a.len, 1u, ulo0, span);
+    } else {  // parts of one root
+      const uint32_t per = (a.len + 63) / 64;
+      tmode[t] = 2u;
+      tu[t] = c0.key;
+      tper[t] = per;
+      tm[t] = msm(a.lo, a.len, 2u, per, 0u);
+    }
+    if (T.fresh) {
+      tyi[t] = t;  // fresh tests come first: y_up element t
+      for (int q = 0; q < 144; q++) yup[(size_t)q * n_fresh + t] = F[T.src].y[q];
     }
   }
-  const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * LB_MSM_NB;
-  const uint32_t bcap = (2 * LB_MSM_W * T) / LB_GROUP_CHUNK + nb;
-  LB_HIP(e->srch_kind.ensure(c * 4));
-  LB_HIP(e->srch_key.ensure(c * 4));
-  LB_HIP(e->srch_lo.ensure(c * 4));
-  LB_HIP(e->srch_len.ensure(c * 4));
-  LB_HIP(e->srch_midx.ensure(c * 4));
-  LB_HIP(e->srch_mlo.ensure((cm + 1) * 4));
-  LB_HIP(e->srch_pre.ensure((cm + 1) * 4));
-  LB_HIP(e->srch_S.ensure((cm ? cm : 1) * sizeof(g2j)));
-  LB_HIP(e->srch_pk.ensure(c * sizeof(g1j)));
-  LB_HIP(e->srch_verdict.ensure(c * 4));
-  LB_HIP(hipMemcpyAsync(e->srch_kind.p, hk.data(), c * 4, hipMemcpyHostToDevice, s1));
-  LB_HIP(hipMemcpyAsync(e->srch_key.p, hkey.data(), c * 4, hipMemcpyHostToDevice, s1));
-  LB_HIP(hipMemcpyAsync(e->srch_lo.p, hlo.data(), c * 4, hipMemcpyHostToDevice, s1));
-  LB_HIP(hipMemcpyAsync(e->srch_len.p, hlen.data(), c * 4, hipMemcpyHostToDevice, s1));
-  LB_HIP(hipMemcpyAsync(e->srch_midx.p, midx.data(), c * 4, hipMemcpyHostToDevice, s1));
+  const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * LB_SMSM_NB;
+  const uint32_t bcap = (2 * LB_SMSM_W * T) / LB_GROUP_CHUNK + nb;
+  LB_HIP(sx_up(e, SX_KIND, dk, s1));
+  LB_HIP(sx_up(e, SX_KEY, dkey, s1));
+  LB_HIP(sx_up(e, SX_LO, dlo, s1));
+  LB_HIP(sx_up(e, SX_LEN, dlen, s1));
+  LB_HIP(sx_up(e, SX_MIDX, dm, s1));
+  LB_HIP(sx_up(e, SX_MPRE, mpre, s1));
+  LB_HIP(sx_up(e, SX_MLO, mlo, s1));
+  LB_HIP(sx_up(e, SX_MMODE, mmode, s1));
+  LB_HIP(sx_up(e, SX_MWA, mwa, s1));
+  LB_HIP(sx_up(e, SX_MWB, mwb, s1));
+  LB_HIP(sx_up(e, SX_TMODE, tmode, s1));
+  LB_HIP(sx_up(e, SX_TF, tf, s1));
+  LB_HIP(sx_up(e, SX_TV0, tv0, s1));
+  LB_HIP(sx_up(e, SX_TU, tu, s1));
+  LB_HIP(sx_up(e, SX_TMIDX, tm, s1));
+  LB_HIP(sx_up(e, SX_TYIDX, tyi, s1));
+  LB_HIP(sx_up(e, SX_TLO, tlo, s1));
+  LB_HIP(sx_up(e, SX_TLEN, tlen, s1));
+  LB_HIP(sx_up(e, SX_TPER, tper, s1));
+  LB_HIP(sx_up(e, SX_YUP, yup, s1));
+  const uint32_t N = c + nt;
+  LB_HIP(e->sx[SX_VERDICT].ensure((c ? c : 1) * 4));
+  LB_HIP(e->sx[SX_Y].ensure((size_t)(N ? N : 1) * 576));
+  LB_HIP(e->sx[SX_ML].ensure((size_t)(N ? N : 1) * 2 * 576));
+  LB_HIP(e->sx[SX_PK].ensure((c ? c : 1) * sizeof(g1j)));
+  LB_HIP(e->sx[SX_S].ensure((cm ? cm : 1) * sizeof(g2j)));
+  LB_HIP(e->sx[SX_TOUT].ensure((nt ? nt : 1) * 4));
+  LB_HIP(e->sx[SX_TPK].ensure((nt ? nt : 1) * sizeof(g1j)));
+  auto U = [&](int k) { return e->sx[k].as<uint32_t>(); };
   {
     stage_scope sc(e, ST_FALLBACK, s1);
     if (cm) {
@@ -753,145 +874,204 @@ static int32_t check_search_nodes(lb_engine* e, const std::vector<search_node>& 
       LB_HIP(e->bch.ensure((size_t)(nb + 1) * 4));
       LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
       LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
-      LB_HIP(e->bmembers.ensure((size_t)2 * LB_MSM_W * (T ? T : 1) * 4));
+      LB_HIP(e->bmembers.ensure((size_t)2 * LB_SMSM_W * (T ? T : 1) * 4));
       LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
       LB_HIP(e->bsum.ensure((size_t)nb * sizeof(g2j)));
-      LB_HIP(hipMemcpyAsync(e->srch_mlo.p, mlo.data(), cm * 4, hipMemcpyHostToDevice, s1));
-      LB_HIP(hipMemcpyAsync(e->srch_pre.p, mpre.data(), (cm + 1) * 4, hipMemcpyHostToDevice, s1));
-      // S of every kind-0/1 node by one range MSM
       LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)nb * 4, s1));
       LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)nb * 4, s1));
-      hipLaunchKernelGGL(k_rmsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, e->srch_pre.as<uint32_t>(),
-                         e->srch_mlo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
-                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+      const smsm_args ma{U(SX_MPRE), U(SX_MLO), U(SX_MMODE), U(SX_MWA), U(SX_MWB)};
+      if (T) {
+        hipLaunchKernelGGL(k_smsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
+                           e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+      }
       hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
                          e->bchunk_end.as<uint32_t>());
-      hipLaunchKernelGGL(k_rmsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, e->srch_pre.as<uint32_t>(),
-                         e->srch_mlo.as<uint32_t>(), e->members.as<uint32_t>(), e->scalars.as<uint64_t>(),
-                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
-                         e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
+      if (T) {
+        hipLaunchKernelGGL(k_smsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
+                           e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(), e->bcursor.as<uint32_t>(),
+                           e->bmembers.as<uint32_t>());
+      }
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
-      hipLaunchKernelGGL(k_msm_reduce, dim3(cm), dim3(64), 0, s1, e->bsum.as<uint32_t>(), nb,
-                         e->srch_S.as<uint32_t>(), cm, 0u);
+      hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(16 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
+                         U(SX_S), cm, 0u);
     }
-    // kind-1 nodes: sum r_i PK_i over the part
-    hipLaunchKernelGGL(k_range_pk, dim3(nblk((uint32_t)c)), dim3(LB_TPB), 0, s1, (uint32_t)c,
-                       e->srch_kind.as<uint32_t>(), e->srch_lo.as<uint32_t>(), e->srch_len.as<uint32_t>(),
-                       e->members.as<uint32_t>(), e->set_live.as<uint32_t>(), n, e->rpk.as<uint32_t>(),
-                       e->srch_pk.as<uint32_t>());
+    if (c)
+      hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),
+                         e->members.as<uint32_t>(), e->set_live.as<uint32_t>(), n, e->rpk.as<uint32_t>(), U(SX_PK));
+    if (nt)
+      hipLaunchKernelGGL(k_test_pk, dim3(nt), dim3(64), 0, s1, nt, U(SX_TMODE), U(SX_TLO), U(SX_TLEN), U(SX_TPER),
+                         e->members.as<uint32_t>(), e->set_live.as<uint32_t>(), n, e->rpk.as<uint32_t>(), U(SX_TPK));
   }
   {
     stage_scope sc(e, ST_BISECT, s1);
-    hipLaunchKernelGGL(k_search_check, dim3((uint32_t)c), dim3(64), 0, s1, (uint32_t)c, e->srch_kind.as<uint32_t>(),
-                       e->srch_key.as<uint32_t>(), e->srch_midx.as<uint32_t>(), cm ? cm : 1u, e->treeP.as<uint32_t>(),
-                       2 * mu, e->srch_pk.as<uint32_t>(), e->h_aff.as<uint32_t>(), n, e->srch_S.as<uint32_t>(),
-                       e->pk_aff.as<uint32_t>(), e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
-                       e->set_live.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->srch_verdict.as<int32_t>());
+    const srch_items I{c, nt, n_fresh, U(SX_KIND), U(SX_KEY), U(SX_MIDX), U(SX_TMODE), U(SX_TF), U(SX_TV0),
+                       U(SX_TU), U(SX_TMIDX), U(SX_TYIDX)};
+    auto stage = [&](uint32_t it0, uint32_t cnt) {
+      if (!cnt) return;
+      hipLaunchKernelGGL(k_search_ml, dim3(2 * cnt), dim3(64), 0, s1, I, it0, cnt, cm ? cm : 1u, e->treeP.as<uint32_t>(),
+                         2 * x.mu, U(SX_PK), U(SX_TPK), e->h_aff.as<uint32_t>(), n, U(SX_S), e->pk_aff.as<uint32_t>(),
+                         e->sig_aff.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->set_live.as<uint32_t>(),
+                         e->set_uid.as<uint32_t>(), U(SX_Y), U(SX_ML));
+      hipLaunchKernelGGL(k_search_fe, dim3(cnt), dim3(64), 0, s1, I, it0, cnt, U(SX_ML), U(SX_Y),
+                         e->sx[SX_VERDICT].as<int32_t>());
+    };
+    stage(0, c + n_fresh);        // direct checks and fresh tests
+    stage(c + n_fresh, nt - n_fresh);  // look-ahead tests of the failing direct checks
+    if (nt) hipLaunchKernelGGL(k_search_match, dim3(nt), dim3(64), 0, s1, I, U(SX_YUP), U(SX_Y), e->sx[SX_TOUT].as<int32_t>());
   }
   LB_HIP(hipGetLastError());
   verdict.resize(c);
-  LB_HIP(hipMemcpyAsync(verdict.data(), e->srch_verdict.p, c * 4, hipMemcpyDeviceToHost, s1));
+  ydir.resize((size_t)144 * N);  // SoA, stride N = c + nt (direct checks first)
+  tout.resize(nt);
+  if (c) {
+    LB_HIP(hipMemcpyAsync(verdict.data(), e->sx[SX_VERDICT].p, (size_t)c * 4, hipMemcpyDeviceToHost, s1));
+    LB_HIP(hipMemcpyAsync(ydir.data(), e->sx[SX_Y].p, (size_t)N * 576, hipMemcpyDeviceToHost, s1));
+  }
+  if (nt) LB_HIP(hipMemcpyAsync(tout.data(), e->sx[SX_TOUT].p, (size_t)nt * 4, hipMemcpyDeviceToHost, s1));
   LB_HIP(hipStreamSynchronize(s1));
+  if (e->profiling)
+    for (int k : {(int)ST_FALLBACK, (int)ST_BISECT}) {
+      float ms = 0.f;
+      if (e->used[k] && hipEventElapsedTime(&ms, e->ev0[k], e->ev1[k]) == hipSuccess) e->acc_ms[k] += ms;
+      e->used[k] = false;
+    }
   return LB_OK;
-}
-
-// Refines a failing node into its children (appended to `out`); a failing single set goes to
-// `bad_pos` (its position in the members array).  Subtrees of the root tree descend to the
-// leaves in steps of at most 2^6 children (the first step from the root: 2^first_step); a
-// failing root with <= 512 members is checked set by set, a bigger one in 64 parts first.
-static void refine(const search_node& f, int32_t fid, uint32_t L, uint32_t nu, const std::vector<uint32_t>& goff,
-                   const std::vector<uint32_t>& members, uint32_t tree_step, std::vector<search_node>& out,
-                   std::vector<uint32_t>& bad_pos) {
-  const uint32_t mu = 1u << L;
-  auto singles = [&](uint32_t lo, uint32_t len) {
-    for (uint32_t q = lo; q < lo + len; q++) out.push_back({2u, members[q], q, 1u, fid});
-  };
-  auto parts = [&](uint32_t u, uint32_t lo, uint32_t len) {
-    const uint32_t per = (len + 63) / 64;
-    for (uint32_t a = 0; a < len; a += per) out.push_back({1u, u, lo + a, (a + per < len ? per : len - a), fid});
-  };
-  if (f.kind == 2) {
-    bad_pos.push_back(f.lo);
-    return;
-  }
-  if (f.kind == 1) {
-    if (f.len <= 512) singles(f.lo, f.len);
-    else parts(f.key, f.lo, f.len);
-    return;
-  }
-  uint32_t d = 0;
-  while ((2u << d) <= f.key) d++;  // depth of heap index key
-  if (d == L) {                    // a leaf: root u's members
-    const uint32_t u = f.key - mu, lo = goff[u], len = goff[u + 1] - goff[u];
-    if (len <= 512) singles(lo, len);
-    else parts(u, lo, len);
-    return;
-  }
-  const uint32_t dd = (L - d <= 6 || d + tree_step >= L) ? L : d + tree_step, k = dd - d;
-  for (uint32_t v = f.key << k; v < (f.key + 1) << k; v++) {
-    const uint32_t span = L - dd, ulo = (v - (1u << dd)) << span;
-    if (ulo >= nu) break;
-    const uint32_t uend = ((v - (1u << dd)) + 1) << span, uhi = uend < nu ? uend : nu;
-    out.push_back({0u, v, goff[ulo], goff[uhi] - goff[ulo], fid});
-  }
 }
 
 static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* out_job) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
-  uint32_t L = 0;
-  while ((1u << L) < mu) L++;
-  const uint32_t nu = *e->h_nu;
-  std::vector<uint32_t> goff(nu + 1), members(n);
-  LB_HIP(hipMemcpyAsync(goff.data(), e->goff.p, (size_t)(nu + 1) * 4, hipMemcpyDeviceToHost, e->stream));
-  LB_HIP(hipMemcpyAsync(members.data(), e->members.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  search_ctx x;
+  x.n = n;
+  x.mu = mu;
+  x.L = 0;
+  while ((1u << x.L) < mu) x.L++;
+  x.nu = *e->h_nu;
+  x.goff.resize(x.nu + 1);
+  x.members.resize(n);
+  fnode root{{0u, 1u, 0u, n, 0u}, true, std::vector<uint32_t>(144)};
+  LB_HIP(hipMemcpyAsync(x.goff.data(), e->goff.p, (size_t)(x.nu + 1) * 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipMemcpyAsync(x.members.data(), e->members.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipMemcpyAsync(root.y.data(), e->y_root.p, 576, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipStreamSynchronize(e->stream));
-  std::vector<search_node> failing{{0u, 1u, 0u, n, -1}};  // the root: known to fail
+  std::vector<fnode> F{root};
   std::vector<uint32_t> bad_pos;
-  const size_t kMaxNodes = 2048, kMaxMsm = 1024;  // per check launch (the MSM's buckets: 1024 per node)
-  bool first = true;
-  while (!failing.empty()) {
-    std::vector<search_node> cand;
-    for (size_t k = 0; k < failing.size(); k++)
-      refine(failing[k], (int32_t)k, L, nu, goff, members, first ? 10 : 6, cand, bad_pos);
-    first = false;
-    if (cand.empty()) break;
-    std::vector<int32_t> v(cand.size()), vk;
-    for (size_t a = 0; a < cand.size();) {
-      // a launch takes up to kMaxNodes nodes, of which at most kMaxMsm need the range MSM
-      size_t c = 0, cm = 0;
-      while (a + c < cand.size() && c < kMaxNodes && (cand[a + c].kind == 2u || cm < kMaxMsm)) {
-        cm += cand[a + c].kind != 2u;
-        c++;
+  auto condemn = [&](const snode& a) {
+    for (uint32_t q = 0; q < a.len; q++) bad_pos.push_back(a.lo + q);
+  };
+  const bool trace = std::getenv("LB_SEARCH_TRACE") != nullptr;
+  const size_t kMaxMsm = 1024;  // MSM instances per launch set (1280 buckets each)
+  std::vector<snode> ch;
+  for (int round = 1; !F.empty(); round++) {
+    if (round > 64) {  // depth is bounded far below this; fail closed if it is ever exceeded
+      for (const fnode& f : F) condemn(f.s);
+      break;
+    }
+    std::vector<fnode> next;
+    // settle single-child chains and terminals on the host
+    std::vector<fnode> work;
+    for (fnode& f : F) {
+      while (true) {
+        if (f.s.len <= 1) {
+          bad_pos.push_back(f.s.lo);
+          break;
+        }
+        search_children(x, f.s, f.multi, ch);
+        if (ch.size() == 1) {
+          f.s = ch[0];
+          f.multi = false;
+          continue;
+        }
+        if (ch.empty()) condemn(f.s);
+        else work.push_back(f);
+        break;
       }
-      int32_t st = check_search_nodes(e, cand, a, c, n, mu, vk);
+    }
+    for (size_t a = 0; a < work.size();) {
+      // a launch set: whole failing nodes until the MSM instance budget is reached
+      std::vector<fnode> Fs;
+      std::vector<snode> D;
+      std::vector<uint32_t> d_owner;  // D index -> Fs index
+      std::vector<test_job> fresh, ahead;
+      size_t inst = 0;
+      while (a < work.size() && (Fs.empty() || inst < kMaxMsm)) {
+        const fnode& f = work[a++];
+        const uint32_t fi = (uint32_t)Fs.size();
+        Fs.push_back(f);
+        if (!f.multi) {
+          test_job t{f.s, {}, true, fi};
+          search_children(x, f.s, false, t.ch);
+          fresh.push_back(std::move(t));
+          inst++;
+          continue;
+        }
+        std::vector<snode> dch;
+        search_children(x, f.s, true, dch);
+        for (const snode& c : dch) {
+          const uint32_t di = (uint32_t)D.size();
+          D.push_back(c);
+          d_owner.push_back(fi);
+          inst += c.kind != 2u;
+          test_job t{c, {}, false, di};
+          search_children(x, c, false, t.ch);
+          if (t.ch.size() >= 2) {
+            ahead.push_back(std::move(t));
+            inst++;
+          }
+        }
+      }
+      std::vector<test_job> tests(fresh);
+      const uint32_t n_fresh = (uint32_t)fresh.size();
+      tests.insert(tests.end(), ahead.begin(), ahead.end());
+      std::vector<int32_t> verdict, tout;
+      std::vector<uint32_t> ydir;
+      const auto t0 = std::chrono::steady_clock::now();
+      const int32_t st = search_round(e, x, Fs, D, tests, n_fresh, verdict, ydir, tout);
       if (st != LB_OK) return st;
-      for (size_t j = 0; j < c; j++) v[a + j] = vk[j];
-      a += c;
-    }
-    // fail closed: a failing node none of whose children fails (impossible for exact arithmetic)
-    // condemns its whole range
-    std::vector<int> child_fail(failing.size(), 0), refined(failing.size(), 0);
-    std::vector<search_node> next;
-    for (size_t j = 0; j < cand.size(); j++) {
-      refined[cand[j].parent] = 1;
-      if (!v[j]) {
-        child_fail[cand[j].parent]++;
-        next.push_back(cand[j]);
+      if (trace)
+        std::fprintf(stderr, "[lb search] round %d: %zu failing nodes, %zu direct checks, %zu weighted tests: %.3f ms\n",
+                     round, Fs.size(), D.size(), tests.size(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      // fresh tests: the named child, or the node again with its children to check directly
+      for (uint32_t t = 0; t < n_fresh; t++) {
+        const fnode& f = Fs[tests[t].src];
+        const int k = tout[t];
+        if (k >= 1 && (size_t)k <= tests[t].ch.size()) next.push_back({tests[t].ch[k - 1], false, f.y});
+        else next.push_back({f.s, true, f.y});
       }
+      // direct checks: each failing child goes on by its weighted test
+      std::vector<int> any_fail(Fs.size(), 0);
+      std::vector<int32_t> ahead_of(D.size(), -1);
+      for (uint32_t t = n_fresh; t < tests.size(); t++) ahead_of[tests[t].src] = (int32_t)t;
+      for (uint32_t j = 0; j < D.size(); j++) {
+        if (verdict[j]) continue;
+        any_fail[d_owner[j]] = 1;
+        std::vector<uint32_t> yc(144);  // y_out is SoA with stride c: gather this node's 144 words
+        for (int q = 0; q < 144; q++) yc[q] = ydir[(size_t)q * (D.size() + tests.size()) + j];
+        const int32_t t = ahead_of[j];
+        if (t < 0) {
+          next.push_back({D[j], false, yc});  // terminal or a single child: settled next round
+          continue;
+        }
+        const int k = tout[t];
+        if (k >= 1 && (size_t)k <= tests[t].ch.size()) next.push_back({tests[t].ch[k - 1], false, yc});
+        else next.push_back({D[j], true, yc});
+      }
+      // fail closed: a multi node none of whose children fails (impossible for exact arithmetic)
+      for (size_t fi = 0; fi < Fs.size(); fi++)
+        if (Fs[fi].multi && !any_fail[fi]) condemn(Fs[fi].s);
     }
-    for (size_t k = 0; k < failing.size(); k++)
-      if (refined[k] && !child_fail[k])
-        for (uint32_t q = 0; q < failing[k].len; q++) bad_pos.push_back(failing[k].lo + q);
-    failing.swap(next);
+    F.swap(next);
   }
   // failing sets -> their jobs (set_live makes every failing set belong to a live job)
   for (uint32_t pos : bad_pos) {
-    const uint32_t i = members[pos];
+    const uint32_t i = x.members[pos];
     const uint32_t j = (uint32_t)(std::upper_bound(b->job_off.begin(), b->job_off.end(), i) - b->job_off.begin()) - 1;
     if (j < nj && out_job[j] == 1) out_job[j] = 0;
   }
@@ -905,7 +1085,7 @@ static void finish_profile(lb_engine* e) {
   for (int k = 0; k < kStages; k++) {
     float ms = 0.f;
     if (e->used[k]) hipEventElapsedTime(&ms, e->ev0[k], e->ev1[k]);
-    e->last_ms[k] = ms;
+    e->last_ms[k] = ms + e->acc_ms[k];
   }
 }
 
@@ -921,8 +1101,9 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   LB_HIP(e->verdict.ensure(4));
   {
     stage_scope sc(e, ST_ROOT, e->stream);
+    LB_HIP(e->y_root.ensure(576));
     hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
-                       e->fS.as<uint32_t>(), e->verdict.as<int32_t>());
+                       e->fS.as<uint32_t>(), e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
   }
   LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(nj);

@@ -632,16 +632,18 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t*
   for (uint32_t c = bch[b]; c < bch[b + 1]; c++) acc = jac_add_i(acc, soa_ld<g2j>(bacc, cap, c));
   soa_st(bsum, nb, b, acc);
 }
-// One wave per MSM instance j (buckets [j LB_MSM_NB, (j+1) LB_MSM_NB) of bsum, stride nb):
-// lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
+// One workgroup per MSM instance j of W windows (buckets [j W 256, (j+1) W 256) of bsum, stride
+// nb): lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
 // Y = sum_j j B_{16s+j} and T = sum_j B_{16s+j}; Y + 16 s T is the segment's share of
 // sum_d d B_d.  Segments then add up in an LDS tree, and the windows combine Horner-style:
-// S = sum_w 2^(8w) W_w  -> element out0 + j of `out` (SoA, stride n_out).
-__global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
-                                                   uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
-  static_assert(LB_MSM_W * 16 == 64 && LB_MSM_B == 256, "one lane per 16-digit segment");
-  __shared__ g2j sh[64];
-  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u, base = blockIdx.x * LB_MSM_NB;
+// S = sum_w 2^(8w) W_w  -> element out0 + j of `out` (SoA, stride n_out).  W = 4 (32-bit
+// scalars) for the batch MSM, 5 for the search's weighted scalars (up to 40 bits).
+template <int W>
+__global__ void __launch_bounds__(16 * W) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                       uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
+  static_assert(LB_MSM_B == 256, "16 lanes of 16 digits per window");
+  __shared__ g2j sh[16 * W];
+  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u, base = blockIdx.x * (W * LB_MSM_B);
   g2j run = jac_infinity<fp2>(), y = jac_infinity<fp2>();
   for (int j = 15; j >= 1; j--) {
     run = jac_add_i(run, soa_ld<g2j>(bsum, nb, base + w * LB_MSM_B + 16 * sg + j));
@@ -663,8 +665,8 @@ __global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ 
     __syncthreads();
   }
   if (lane == 0) {
-    g2j S = sh[16 * (LB_MSM_W - 1)];
-    for (int ww = LB_MSM_W - 2; ww >= 0; ww--) {
+    g2j S = sh[16 * (W - 1)];
+    for (int ww = W - 2; ww >= 0; ww--) {
       for (int b = 0; b < LB_MSM_C; b++) S = jac_dbl_i(S);
       S = jac_add_i(S, sh[16 * ww]);
     }
@@ -682,8 +684,15 @@ __global__ void __launch_bounds__(64) k_msm_reduce(const uint32_t* __restrict__ 
 //          no blinding and no MSM (a set of a rejected job passes trivially).
 // By bilinearity a node's verdict is the product of its children's, so a failing node has a
 // failing child; the host descends until single sets (lb_engine.hip search_invalid).
-// Range MSM for S_j: every (set, window) digit of node j joins bucket j LB_MSM_NB + w 256 + d.
-// Thread t of the T = sum len_j member positions finds its node by binary search of pre[].
+// Search MSM: instance j covers member positions [lo_j, lo_j + len_j) (thread t of the
+// T = sum len_j positions finds its instance by binary search of pre[]) with the scalar of set i
+// multiplied by a small weight: mode 0 weight 1 (S of a node), mode 1 (a weighted test over
+// subtrees of 2^b roots from root a) weight ((set_uid_i - a) >> b) + 1, mode 2 (a weighted test
+// over parts of a members) weight (position offset / a) + 1.  Weights are <= 128, so both
+// 32-bit GLV halves of r_i w stay below 2^40: LB_SMSM_W = 5 windows of 8 bits, instance j owning
+// buckets [j LB_SMSM_NB, (j+1) LB_SMSM_NB).
+#define LB_SMSM_W 5
+#define LB_SMSM_NB (LB_SMSM_W * LB_MSM_B)
 __device__ __forceinline__ uint32_t rmsm_node(const uint32_t* __restrict__ pre, uint32_t c, uint32_t t) {
   uint32_t lo = 0, hi = c;  // pre[lo] <= t < pre[hi]
   while (hi - lo > 1) {
@@ -693,29 +702,44 @@ __device__ __forceinline__ uint32_t rmsm_node(const uint32_t* __restrict__ pre, 
   }
   return lo;
 }
-__global__ void __launch_bounds__(LB_TPB) k_rmsm_count(uint32_t T, uint32_t c, const uint32_t* __restrict__ pre,
-                                                       const uint32_t* __restrict__ rlo,
+struct smsm_args {
+  const uint32_t *pre, *rlo, *mode, *wa, *wb;
+};
+__device__ __forceinline__ bool smsm_member(const smsm_args& a, uint32_t c, uint32_t t,
+                                            const uint32_t* __restrict__ members,
+                                            const uint32_t* __restrict__ set_uid, uint32_t& j, uint32_t& i,
+                                            uint32_t& wt) {
+  j = rmsm_node(a.pre, c, t);
+  const uint32_t off = t - a.pre[j];
+  i = members[a.rlo[j] + off];
+  const uint32_t md = a.mode[j];
+  wt = md == 0u ? 1u : (md == 1u ? ((set_uid[i] - a.wa[j]) >> a.wb[j]) + 1u : off / a.wa[j] + 1u);
+  return true;
+}
+__global__ void __launch_bounds__(LB_TPB) k_smsm_count(uint32_t T, uint32_t c, smsm_args a,
                                                        const uint32_t* __restrict__ members,
+                                                       const uint32_t* __restrict__ set_uid,
                                                        const uint64_t* __restrict__ scalars,
                                                        const uint32_t* __restrict__ set_live,
                                                        const uint32_t* __restrict__ sig_inf,
                                                        uint32_t* __restrict__ cnt) {
   const uint32_t t = lb_tid();
   if (t >= T) return;
-  const uint32_t j = rmsm_node(pre, c, t), i = members[rlo[j] + t - pre[j]];
+  uint32_t j, i, wt;
+  smsm_member(a, c, t, members, set_uid, j, i, wt);
   if (!msm_live(i, set_live, sig_inf)) return;
   const uint64_t wd = scalars[i];
   LB_UNROLL for (int h = 0; h < 2; h++) {
-    const uint32_t k = (uint32_t)(wd >> (32 * h));
-    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
-      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
-      if (d) atomicAdd(&cnt[j * LB_MSM_NB + w * LB_MSM_B + d], 1u);
+    const uint64_t k = (uint64_t)(uint32_t)(wd >> (32 * h)) * wt;
+    LB_UNROLL for (int w = 0; w < LB_SMSM_W; w++) {
+      const uint32_t d = (uint32_t)(k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+      if (d) atomicAdd(&cnt[j * LB_SMSM_NB + w * LB_MSM_B + d], 1u);
     }
   }
 }
-__global__ void __launch_bounds__(LB_TPB) k_rmsm_scatter(uint32_t T, uint32_t c, const uint32_t* __restrict__ pre,
-                                                         const uint32_t* __restrict__ rlo,
+__global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c, smsm_args a,
                                                          const uint32_t* __restrict__ members,
+                                                         const uint32_t* __restrict__ set_uid,
                                                          const uint64_t* __restrict__ scalars,
                                                          const uint32_t* __restrict__ set_live,
                                                          const uint32_t* __restrict__ sig_inf,
@@ -723,22 +747,23 @@ __global__ void __launch_bounds__(LB_TPB) k_rmsm_scatter(uint32_t T, uint32_t c,
                                                          uint32_t* __restrict__ cursor, uint32_t* __restrict__ bmembers) {
   const uint32_t t = lb_tid();
   if (t >= T) return;
-  const uint32_t j = rmsm_node(pre, c, t), i = members[rlo[j] + t - pre[j]];
+  uint32_t j, i, wt;
+  smsm_member(a, c, t, members, set_uid, j, i, wt);
   if (!msm_live(i, set_live, sig_inf)) return;
   const uint64_t wd = scalars[i];
   LB_UNROLL for (int h = 0; h < 2; h++) {
-    const uint32_t k = (uint32_t)(wd >> (32 * h));
-    LB_UNROLL for (int w = 0; w < LB_MSM_W; w++) {
-      const uint32_t d = (k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
+    const uint64_t k = (uint64_t)(uint32_t)(wd >> (32 * h)) * wt;
+    LB_UNROLL for (int w = 0; w < LB_SMSM_W; w++) {
+      const uint32_t d = (uint32_t)(k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
       if (d) {
-        const uint32_t b = j * LB_MSM_NB + w * LB_MSM_B + d;
+        const uint32_t b = j * LB_SMSM_NB + w * LB_MSM_B + d;
         bmembers[boff[b] + atomicAdd(&cursor[b], 1u)] = i | ((uint32_t)h << 31);
       }
     }
   }
 }
-// kind-1 nodes: Jacobian sum of r_i PK_i over the node's live members -> pk_out (SoA, stride c);
-// the range MSM (k_rmsm_*, instance m = midx of a kind-0/1 node) writes S_m to s_out (stride cm)
+// direct kind-1 nodes: Jacobian sum of r_i PK_i over the part's live members -> pk_out (SoA,
+// stride c)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,
                                                        const uint32_t* __restrict__ rlo,
                                                        const uint32_t* __restrict__ rlen,
@@ -754,76 +779,76 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, c
   }
   soa_st(pk_out, c, j, acc);
 }
-// One wave per node: verdict[j] = FE(P_j * ML(-G1, S_j)) == 1 (Pairing.finalverify)
-__global__ void __launch_bounds__(64) k_search_check(uint32_t c, const uint32_t* __restrict__ kind,
-                                                     const uint32_t* __restrict__ key,
-                                                     const uint32_t* __restrict__ midx, uint32_t cm,
-                                                     const uint32_t* __restrict__ treeP, uint32_t n2m,
-                                                     const uint32_t* __restrict__ pk_out,
-                                                     const uint32_t* __restrict__ h_aff, uint32_t n,
-                                                     const uint32_t* __restrict__ s_out,
-                                                     const uint32_t* __restrict__ pk_aff,
-                                                     const uint32_t* __restrict__ sig_aff,
-                                                     const uint32_t* __restrict__ sig_inf,
-                                                     const uint32_t* __restrict__ set_live,
-                                                     const uint32_t* __restrict__ set_uid,
-                                                     int32_t* __restrict__ verdict) {
-  LBW_SHARED(S);
+// weighted tests over parts of one root (mode 2): sum_k (k + 1) sum_{i in part k} r_i PK_i,
+// one workgroup per test, lane k < f owning part k (64 lanes, two parts per lane above 64)
+__global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __restrict__ mode,
+                                                const uint32_t* __restrict__ tlo, const uint32_t* __restrict__ tlen,
+                                                const uint32_t* __restrict__ per, const uint32_t* __restrict__ members,
+                                                const uint32_t* __restrict__ set_live, uint32_t n,
+                                                const uint32_t* __restrict__ rpk, uint32_t* __restrict__ pk_out) {
+  __shared__ g1j sh[64];
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  if (t >= nt || mode[t] != 2u) return;
+  const uint32_t lo = tlo[t], len = tlen[t], pp = per[t];
+  g1j tot = jac_infinity<fp>();
+  for (uint32_t k = lane; k * pp < len; k += 64) {
+    g1j acc = jac_infinity<fp>();
+    const uint32_t a = lo + k * pp, e = lo + (k * pp + pp < len ? k * pp + pp : len);
+    for (uint32_t q = a; q < e; q++) {
+      const uint32_t i = members[q];
+      if (set_live[i]) acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));
+    }
+    g1j m = jac_infinity<fp>();
+    const uint32_t wt = k + 1;
+    for (int b = 7; b >= 0; b--) {
+      m = jac_dbl_i(m);
+      if ((wt >> b) & 1u) m = jac_add_i<fp, true>(m, acc);
+    }
+    tot = jac_add_i<fp, true>(tot, m);
+  }
+  sh[lane] = tot;
+  __syncthreads();
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    if (lane < d) sh[lane] = jac_add_i<fp, true>(sh[lane], sh[lane + d]);
+    __syncthreads();
+  }
+  if (lane == 0) soa_st(pk_out, nt, t, sh[0]);
+}
+
+// ML(PK, H_u) of a G1 Jacobian point into area dst (1 for infinity); lane 0 stages the points
+__device__ void w_miller_pk(fp* S, int dst, const g1j& pj_lane0, const uint32_t* __restrict__ h_aff, uint32_t n,
+                            uint32_t u) {
   __shared__ int s_inf;
-  const uint32_t j = blockIdx.x;
-  if (j >= c) return;
-  const int lane = threadIdx.x;
-  const uint32_t kd = kind[j];
-  if (kd == 2u && !set_live[key[j]]) {  // a set of a rejected job takes no part
-    if (lane == 0) verdict[j] = 1;
-    return;
-  }
-  w_init_consts(S);
-  if (kd == 0u) {
-    w_load_soa12(S, LBW_A(0), treeP, n2m, key[j]);
-  } else {
-    if (lane == 0) {
-      g1j pj;
-      uint32_t u;
-      if (kd == 1u) {
-        pj = soa_ld<g1j>(pk_out, c, j);
-        u = key[j];
-      } else {
-        pj = jac_from_aff(soa_ld<g1a>(pk_aff, n, key[j]));
-        u = set_uid[key[j]];
-      }
-      s_inf = jac_is_inf(pj) ? 1 : 0;
-      if (!s_inf) {
-        g1a pa;
-        jac_to_aff(pa, pj);
-        const g2a h = soa_ld<g2a>(h_aff, n, u);
-        w_st(S, LBW_PT + 0, pa.x);
-        w_st(S, LBW_PT + 1, pa.y);
-        w_st(S, LBW_PT + 2, h.x.c0);
-        w_st(S, LBW_PT + 3, h.x.c1);
-        w_st(S, LBW_PT + 4, h.y.c0);
-        w_st(S, LBW_PT + 5, h.y.c1);
-      }
-    }
-    w_sync();
-    const int inf = s_inf;
-    w_sync();
-    if (inf)
-      w_set_one(S, LBW_A(0));
-    else
-      w_miller(S, LBW_A(0));
-  }
-  if (lane == 0) {
-    g2a a;
-    if (kd == 2u) {
-      s_inf = sig_inf[key[j]] ? 1 : 0;
-      a = soa_ld<g2a>(sig_aff, n, key[j]);
-    } else {
-      const g2j Sj = soa_ld<g2j>(s_out, cm, midx[j]);
-      s_inf = jac_is_inf(Sj) ? 1 : 0;
-      if (!s_inf) jac_to_aff(a, Sj);
-    }
+  if (w_lane() == 0) {
+    s_inf = jac_is_inf(pj_lane0) ? 1 : 0;
     if (!s_inf) {
+      g1a pa;
+      jac_to_aff(pa, pj_lane0);
+      const g2a h = soa_ld<g2a>(h_aff, n, u);
+      w_st(S, LBW_PT + 0, pa.x);
+      w_st(S, LBW_PT + 1, pa.y);
+      w_st(S, LBW_PT + 2, h.x.c0);
+      w_st(S, LBW_PT + 3, h.x.c1);
+      w_st(S, LBW_PT + 4, h.y.c0);
+      w_st(S, LBW_PT + 5, h.y.c1);
+    }
+  }
+  w_sync();
+  const int inf = s_inf;
+  w_sync();
+  if (inf)
+    w_set_one(S, dst);
+  else
+    w_miller(S, dst);
+}
+// ML(-G1, Q) of a G2 Jacobian point into area dst (1 for infinity)
+__device__ void w_miller_negg1(fp* S, int dst, const g2j& q_lane0) {
+  __shared__ int s_inf;
+  if (w_lane() == 0) {
+    s_inf = jac_is_inf(q_lane0) ? 1 : 0;
+    if (!s_inf) {
+      g2a a;
+      jac_to_aff(a, q_lane0);
       w_st(S, LBW_PT + 0, fp_load(LB_G1X));
       w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
       w_st(S, LBW_PT + 2, a.x.c0);
@@ -833,15 +858,163 @@ __global__ void __launch_bounds__(64) k_search_check(uint32_t c, const uint32_t*
     }
   }
   w_sync();
-  const int sinf = s_inf;
+  const int inf = s_inf;
   w_sync();
-  if (!sinf) {
-    w_miller(S, LBW_A(7));
-    w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
+  if (inf)
+    w_set_one(S, dst);
+  else
+    w_miller(S, dst);
+}
+__device__ bool w_eq(fp* S, int a, int b) {
+  __shared__ int diff;
+  if (w_lane() == 0) diff = 0;
+  w_sync();
+  if (w_lane() < 12 && !fp_eq(w_ld(S, a + w_lane()), w_ld(S, b + w_lane()))) atomicOr(&diff, 1);
+  w_sync();
+  const int r = diff;
+  w_sync();
+  return r == 0;
+}
+
+// One search round runs three launches over its items (direct checks first, then weighted
+// tests), one wave each:
+//   k_search_ml     two blocks per item: side 0 the P factor, side 1 ML(-G1, S);
+//   k_search_fe     y_i = FE(P_i ML(-G1, S_i)), verdict of a direct check = (y_i == 1);
+//   k_search_match  a test's z = y_{c+t} against the powers of its node's y.
+// Direct check j (y_j = FE(X_j), Pairing.finalverify):
+//   kind 0 (a subtree of the root product tree, whole roots): P_j = treeP[key_j];
+//   kind 1 (part of one root u = key_j): P_j = ML(sum r_i PK_i, H(m_u)), S_j from the range MSM;
+//   kind 2 (one set i = key_j): Signature.verify itself, FE(ML(PK_i, H(m_i)) ML(-G1, sig_i)),
+//          no blinding and no MSM (a set of a rejected job passes trivially).
+// Weighted test t over the f children of a failing node whose FE value y is known: with weights
+// w_k = k + 1, z = FE(prod_k P_k^{w_k} ML(-G1, sum_k w_k S_k)) = prod_k y_k^{w_k}, so when
+// exactly one child k* fails (y_k* = y), z = y^{k*+1} and the match returns k* + 1; it returns
+// 0 when z is no power y^1..y^f (two or more failing children: the caller checks them directly).
+// A wrong match needs prod over the other failing children of y_k^{w_k - w_k*} = 1, which the
+// secret blinding scalars make as unlikely (2^-64) as a passing batch with an invalid set.
+//   mode 1: the children are f consecutive nodes v0 + k of the root product tree: P side
+//           prod_k treeP[v0 + k]^{k+1} by running products (2f Fp12 multiplications);
+//   mode 2: the children are parts of root u: P side ML(sum_k (k+1) PKsum_k, H_u) (k_test_pk).
+// A look-ahead test (t >= n_fresh) belongs to direct check tyidx[t] of the same round and is
+// skipped when that check passed (its y is 1): launched after k_search_fe of the direct checks.
+struct srch_items {
+  uint32_t c, nt, n_fresh;
+  const uint32_t *kind, *key, *dmidx;                     // direct checks
+  const uint32_t *tmode, *tf, *tv0, *tu, *tmidx, *tyidx;  // weighted tests
+};
+__device__ bool srch_skip(fp* S, const srch_items& I, uint32_t it, const uint32_t* __restrict__ ybuf) {
+  if (it < I.c + I.n_fresh) return false;
+  w_load_soa12(S, LBW_A(6), ybuf, I.c + I.nt, I.tyidx[it - I.c]);
+  return w_is_one(S, LBW_A(6));
+}
+__global__ void __launch_bounds__(64) k_search_ml(srch_items I, uint32_t it0, uint32_t cnt, uint32_t cm,
+                                                  const uint32_t* __restrict__ treeP, uint32_t n2m,
+                                                  const uint32_t* __restrict__ pk_d, const uint32_t* __restrict__ pk_t,
+                                                  const uint32_t* __restrict__ h_aff, uint32_t n,
+                                                  const uint32_t* __restrict__ s_out,
+                                                  const uint32_t* __restrict__ pk_aff,
+                                                  const uint32_t* __restrict__ sig_aff,
+                                                  const uint32_t* __restrict__ sig_inf,
+                                                  const uint32_t* __restrict__ set_live,
+                                                  const uint32_t* __restrict__ set_uid,
+                                                  const uint32_t* __restrict__ ybuf, uint32_t* __restrict__ ml) {
+  LBW_SHARED(S);
+  if (blockIdx.x >= 2 * cnt) return;
+  const uint32_t it = it0 + (blockIdx.x >> 1), side = blockIdx.x & 1u, N2 = 2 * (I.c + I.nt);
+  const int lane = threadIdx.x;
+  w_init_consts(S);
+  if (srch_skip(S, I, it, ybuf)) {
+    w_set_one(S, LBW_A(0));
+  } else if (it < I.c) {
+    const uint32_t kd = I.kind[it], k = I.key[it];
+    if (kd == 2u && !set_live[k]) {  // a set of a rejected job takes no part
+      w_set_one(S, LBW_A(0));
+    } else if (side == 0) {
+      if (kd == 0u) {
+        w_load_soa12(S, LBW_A(0), treeP, n2m, k);
+      } else {
+        g1j pj;
+        uint32_t u = 0;
+        if (lane == 0) {
+          pj = kd == 1u ? soa_ld<g1j>(pk_d, I.c, it) : jac_from_aff(soa_ld<g1a>(pk_aff, n, k));
+          u = kd == 1u ? k : set_uid[k];
+        }
+        w_miller_pk(S, LBW_A(0), pj, h_aff, n, u);
+      }
+    } else {
+      g2j q;
+      if (lane == 0) {
+        if (kd == 2u) q = sig_inf[k] ? jac_infinity<fp2>() : jac_from_aff(soa_ld<g2a>(sig_aff, n, k));
+        else q = soa_ld<g2j>(s_out, cm, I.dmidx[it]);
+      }
+      w_miller_negg1(S, LBW_A(0), q);
+    }
+  } else {
+    const uint32_t t = it - I.c;
+    if (side == 0) {
+      if (I.tmode[t] == 1u) {
+        const uint32_t v0 = I.tv0[t];
+        w_set_one(S, LBW_A(0));
+        w_set_one(S, LBW_A(1));
+        for (int k = (int)I.tf[t] - 1; k >= 0; k--) {
+          w_load_soa12(S, LBW_A(2), treeP, n2m, v0 + (uint32_t)k);
+          w_mul(S, LBW_A(1), LBW_A(1), LBW_A(2));
+          w_mul(S, LBW_A(0), LBW_A(0), LBW_A(1));
+        }
+      } else {
+        g1j pj;
+        if (lane == 0) pj = soa_ld<g1j>(pk_t, I.nt, t);
+        w_miller_pk(S, LBW_A(0), pj, h_aff, n, I.tu[t]);
+      }
+    } else {
+      g2j q;
+      if (lane == 0) q = soa_ld<g2j>(s_out, cm, I.tmidx[t]);
+      w_miller_negg1(S, LBW_A(0), q);
+    }
   }
-  w_final_exp(S, LBW_A(0), LBW_A(0));
+  w_store_soa12(S, LBW_A(0), ml, N2, 2 * it + side);
+}
+__global__ void __launch_bounds__(64) k_search_fe(srch_items I, uint32_t it0, uint32_t cnt,
+                                                  const uint32_t* __restrict__ ml, uint32_t* __restrict__ ybuf,
+                                                  int32_t* __restrict__ verdict) {
+  LBW_SHARED(S);
+  if (blockIdx.x >= cnt) return;
+  const uint32_t it = it0 + blockIdx.x, N = I.c + I.nt;
+  w_init_consts(S);
+  if (srch_skip(S, I, it, ybuf)) {
+    w_set_one(S, LBW_A(0));
+  } else {
+    w_load_soa12(S, LBW_A(0), ml, 2 * N, 2 * it);
+    w_load_soa12(S, LBW_A(7), ml, 2 * N, 2 * it + 1);
+    w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
+    w_final_exp(S, LBW_A(0), LBW_A(0));
+  }
   const bool one = w_is_one(S, LBW_A(0));
-  if (lane == 0) verdict[j] = one ? 1 : 0;
+  w_store_soa12(S, LBW_A(0), ybuf, N, it);
+  if (threadIdx.x == 0 && it < I.c) verdict[it] = one ? 1 : 0;
+}
+__global__ void __launch_bounds__(64) k_search_match(srch_items I, const uint32_t* __restrict__ y_up,
+                                                     const uint32_t* __restrict__ ybuf, int32_t* __restrict__ out_k) {
+  LBW_SHARED(S);
+  const uint32_t t = blockIdx.x;
+  if (t >= I.nt) return;
+  const uint32_t N = I.c + I.nt, f = I.tf[t];
+  w_init_consts(S);
+  if (t < I.n_fresh) w_load_soa12(S, LBW_A(7), y_up, I.n_fresh, t);
+  else w_load_soa12(S, LBW_A(7), ybuf, N, I.tyidx[t]);
+  if (w_is_one(S, LBW_A(7))) {
+    if (threadIdx.x == 0) out_k[t] = 0;
+    return;
+  }
+  w_load_soa12(S, LBW_A(0), ybuf, N, I.c + t);
+  if (t < I.n_fresh) w_load_soa12(S, LBW_A(1), y_up, I.n_fresh, t);
+  else w_load_soa12(S, LBW_A(1), ybuf, N, I.tyidx[t]);
+  int hit = 0;
+  for (uint32_t k = 1; k <= f && !hit; k++) {
+    if (w_eq(S, LBW_A(0), LBW_A(1))) hit = (int)k;
+    else if (k < f) w_mul(S, LBW_A(1), LBW_A(1), LBW_A(7));
+  }
+  if (threadIdx.x == 0) out_k[t] = hit;
 }
 
 // ---------------------------------------------------------------- per-job leaves
@@ -979,8 +1152,10 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
 }
 
 // root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
+// (the FE value y goes to y_out for the invalid-set search)
 __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
-                                                   const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict) {
+                                                   const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
+                                                   uint32_t* __restrict__ y_out) {
   LBW_SHARED(S);
   w_init_consts(S);
   w_load_soa12(S, LBW_A(0), treeP, 2 * m, 1);
@@ -988,6 +1163,7 @@ __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* _
   w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   w_final_exp(S, LBW_A(0), LBW_A(0));
   bool one = w_is_one(S, LBW_A(0));
+  w_store_soa12(S, LBW_A(0), y_out, 1, 0);
   if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
 

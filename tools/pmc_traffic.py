@@ -1,36 +1,63 @@
 """profiles/traffic.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py at one
-batch in flight: per kernel, average (FETCH_SIZE + WRITE_SIZE) x 1024 bytes per launch.
+batch in flight: per kernel, average (FETCH_SIZE + WRITE_SIZE) x 1024 bytes per launch, and per
+pipeline stage (bench.py roofline), the bytes of all the stage's kernel launches per batch
+(batches = launches of k_decompress_sigs, one per batch).
 
 FETCH_SIZE / WRITE_SIZE are in KB (L2 <-> fabric).  MI355X_MICROARCH.md: FETCH_SIZE under-reports
 wide (16 B/lane) streaming reads by 2x; these kernels read 4-byte SoA words and scratch, an
 uncalibrated width, so the raw value is reported.
 
-  python tools/pmc_traffic.py FETCH.csv WRITE.csv SETS_PER_LAUNCH > profiles/traffic.json
+  python tools/pmc_traffic.py FETCH.csv WRITE.csv SETS_PER_BATCH > profiles/traffic.json
 """
 import collections
 import csv
 import json
 import sys
 
+# bench.py stage -> the kernels its stage_scope brackets (lb_engine.hip run_pipeline)
+STAGES = {
+    "decode_sigs": ["k_decompress_sigs", "k_sig_subgroup", "k_job_status"],
+    "dedup": ["k_msg_insert", "k_msg_count", "k_msg_scatter"],
+    "hash_map": ["k_hash_map"],
+    "hash_finish": ["k_hash_finish"],
+    "pk_chunks": ["k_pk_chunks", "k_pk_chunks_idx"],
+    "pk_blind": ["k_pk_blind"],
+    "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
+    "group_sum": ["k_gsum_chunks", "k_gsum_final"],
+    "miller": ["k_miller_grouped"],
+    "tree_up_P": ["k_tree_up_U"],
+    "ml_S": ["k_ml_S"],
+    "root_check": ["k_root_check"],
+}
+
 
 def per_kernel(path, counter):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in d.items()}
+            name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+            d[name].append(float(r["Counter_Value"]))
+    return d
 
 
 def main():
     fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
     n = int(sys.argv[3])
     out = {"source": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE (separate passes), bench.py --inflight 1",
-           "unit": "bytes per launch", "kernels": {}}
+           "unit": "bytes per launch (kernels) / per batch (stages)", "kernels": {}, "stages": {}}
     for k in sorted(set(fetch) & set(write)):
         if not k.startswith("k_"):
             continue
-        out["kernels"][k] = {"fetch_bytes": round(fetch[k] * 1024), "write_bytes": round(write[k] * 1024),
-                             "bytes_per_launch": round((fetch[k] + write[k]) * 1024), "sets_per_launch": n}
+        f, w = fetch[k], write[k]
+        out["kernels"][k] = {"launches": len(f), "fetch_bytes": round(sum(f) / len(f) * 1024),
+                             "write_bytes": round(sum(w) / len(w) * 1024),
+                             "bytes_per_launch": round((sum(f) / len(f) + sum(w) / len(w)) * 1024)}
+    batches = len(fetch.get("k_decompress_sigs", [])) or 1
+    for st, ks in STAGES.items():
+        tot = sum(sum(fetch.get(k, [])) + sum(write.get(k, [])) for k in ks)
+        if tot:
+            out["stages"][st] = {"kernels": [k for k in ks if k in fetch], "bytes_per_launch": round(tot * 1024 / batches),
+                                 "sets_per_launch": n, "batches": batches}
     json.dump(out, sys.stdout, indent=1)
 
 
