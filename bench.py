@@ -191,6 +191,15 @@ def median_ms(fn, reps):
     return round(float(np.median(ts)), 3)
 
 
+def profiled_stages(eng, fn):
+    """per-stage HIP-event times (ms) of one profiled call"""
+    eng.set_profiling(True)
+    fn()
+    prof = eng.last_profile()
+    eng.set_profiling(False)
+    return {k: round(v, 3) for k, v in prof.items() if v > 0}
+
+
 def extra_legs(a, engs, barrier, W):
     """Secondary measurements (rank 0 at N = 1; each bounded to a few seconds)."""
     out = {}
@@ -225,6 +234,7 @@ def extra_legs(a, engs, barrier, W):
     lat = median_ms(lambda: b1.verify(), max(3, a.steps))
     out["value_slots1"] = round(w1.packed.n_sets / (lat * 1e-3), 1)
     out["latency_slot1_ms"] = lat
+    out["slots1_stage_ms"] = profiled_stages(eng, b1.verify)
     b1.free()
     # small calls through the workspace path (lb_verify_jobs_indexed: upload + verify + readback)
     wc1 = W.make(eng, "c1")
@@ -233,6 +243,7 @@ def extra_legs(a, engs, barrier, W):
                        msgs=ip.msgs[:32], sigs=ip.sigs[:96], sig_sizes=None, pk_indices=ip.pk_indices[:1])
     assert eng.verify_jobs_packed(one) == [1]
     out["latency_1set_ms"] = median_ms(lambda: eng.verify_jobs_packed(one), 10)
+    out["latency_1set_stage_ms"] = profiled_stages(eng, lambda: eng.verify_jobs_packed(one))
     wc2 = W.make(eng, "c2")
     ip2 = W.indexed_for(eng, wc2)
     assert eng.verify_jobs_packed(ip2) == list(wc2.expected)

@@ -116,6 +116,9 @@ struct lb_engine {
   dbuf pk_aff;  // affine aggregate pubkey per set (single-set checks of the search)
   dbuf y_root;  // FE value of the root check (the search starts from it)
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
+  // batches with at most this many distinct roots run their Miller loops one wave per root
+  // (k_miller_wave); larger ones one lane per root (k_miller_grouped).  LB_MILLER_WAVE_MAX.
+  uint32_t miller_wave_max = 2048;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -235,6 +238,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   // so its few-wave kernels are dispatched ahead of the other batches' wide ones
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+  if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -673,8 +677,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_MILLER, s1);
-      hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
-                         e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+      if (nuh <= e->miller_wave_max)
+        hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
     }
     {
       stage_scope sc(e, ST_TREE_P, s1);

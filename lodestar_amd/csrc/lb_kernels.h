@@ -426,6 +426,37 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller_grouped(uint32_t n, 
   soa_st(treeP, 2 * m, m + u, f);
 }
 
+// The same loops one wave per root (w_miller: the doubling / addition steps as wave programs,
+// their ~100 Fp products spread over the lanes).  A lone lane runs a Miller loop's 6 664 serial
+// Fp products in ~12 ms whatever the batch, so for a batch with few distinct roots (one slot of
+// gossip, one block, a single set) this cuts the per-root chain; k_miller_grouped stays the
+// throughput form for large batches (64 roots per wave).  Lanes 0-5 stage P_u (2 Fp) and H(m_u)
+// (4 Fp) from the SoA arrays.
+__global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
+                                                    const uint32_t* __restrict__ gp_aff,
+                                                    const uint32_t* __restrict__ gp_inf,
+                                                    const uint32_t* __restrict__ h_aff, uint32_t* __restrict__ treeP) {
+  LBW_SHARED_MILLER(S);
+  const uint32_t u = blockIdx.x;
+  if (u >= *n_u) return;
+  const int lane = threadIdx.x;
+  w_init_consts(S, LBW_MILLER_COUNT, LBW_MILLER_FIRST);
+  const bool inf = gp_inf[u] != 0;  // uniform
+  if (inf) {
+    w_set_one(S, LBW_A(0));
+  } else {
+    if (lane < 6) {
+      const uint32_t* base = lane < 2 ? gp_aff + (size_t)12 * lane * n : h_aff + (size_t)12 * (lane - 2) * n;
+      fp v;
+      LB_UNROLL for (int w = 0; w < 12; w++) v.v[w] = base[(size_t)w * n + u];
+      w_st(S, LBW_PT + lane, v);
+    }
+    w_sync();
+    w_miller(S, LBW_A(0));
+  }
+  w_store_soa12(S, LBW_A(0), treeP, 2 * m, m + u);
+}
+
 // ---------------------------------------------------------------- message grouping
 // Sets that sign the same 32-byte root share one hash_to_G2 and one Miller loop (on mainnet a
 // committee's unaggregated attestations all sign one AttestationData root, every aggregator of a
@@ -918,11 +949,11 @@ __global__ void __launch_bounds__(64) k_search_ml(srch_items I, uint32_t it0, ui
                                                   const uint32_t* __restrict__ set_live,
                                                   const uint32_t* __restrict__ set_uid,
                                                   const uint32_t* __restrict__ ybuf, uint32_t* __restrict__ ml) {
-  LBW_SHARED(S);
+  LBW_SHARED_ML(S);
   if (blockIdx.x >= 2 * cnt) return;
   const uint32_t it = it0 + (blockIdx.x >> 1), side = blockIdx.x & 1u, N2 = 2 * (I.c + I.nt);
   const int lane = threadIdx.x;
-  w_init_consts(S);
+  w_init_consts(S, LBW_PROGS_ALL);
   if (srch_skip(S, I, it, ybuf)) {
     w_set_one(S, LBW_A(0));
   } else if (it < I.c) {
@@ -1125,10 +1156,10 @@ __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const
 // fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
 // computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
 __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
-  LBW_SHARED(S);
+  LBW_SHARED_ML(S);
   __shared__ int s_inf;
   const int lane = threadIdx.x;
-  w_init_consts(S);
+  w_init_consts(S, LBW_PROGS_ALL);
   if (lane == 0) {
     g2j Sj = soa_ld<g2j>(treeS, 2 * m, 1);
     s_inf = jac_is_inf(Sj) ? 1 : 0;

@@ -31,7 +31,9 @@ by conditional subtraction of 2^j p for every 2^j < B.
 The program encoding is validated here by a Python interpreter against direct big-integer
 evaluation of the same tower formulas (and, through the engine tests, against the oracle).
 """
+import math
 import os
+from fractions import Fraction
 import random
 import sys
 
@@ -44,6 +46,8 @@ PREC = 48    # product record: dst + 2 x MAXP pairs, padded to a 16-byte multipl
 LREC = 56    # linear record: dst + MAXL pairs, padded
 IN_BASE, CONST_BASE, TEMP_BASE = 0, 32, 64
 C_B3, C_INV2, C_FROB1, C_FROB2, C_ZERO = 0, 2, 3, 13, 18   # offsets in CONST
+OUT_FLAG = 0x4000  # on a linear task's dst: a program output, reduced below p
+INV_P320 = float(Fraction(2 ** 320, P))  # nearest double; emitted as a hex literal, so host and device agree
 N_CONST = 19
 
 
@@ -187,7 +191,8 @@ class Prog:
                 npa, nna = max(len(p) for p, _ in ls), max(len(n) for _, n in ls)
                 out += [kind, len(tasks), npa, nna, 0, 0, red(ls), 0]
                 for t, l in zip(tasks, ls):
-                    rec = [t[2]] + pack(l, npa, nna, MAXL)
+                    # program outputs are reduced below p (OUT_FLAG on dst); other temps stay < 3p
+                    rec = [t[2] | (OUT_FLAG if t[2] in self.outs else 0)] + pack(l, npa, nna, MAXL)
                     out += rec + [0] * (LREC - len(rec))
         for v in out:
             assert -32768 <= v < 32768
@@ -393,25 +398,37 @@ def build_programs():
 
 
 # ------------------------------------------------------------ reference evaluation (big ints)
+def quotient_estimate(pa, na):
+    """lb_wave.h w_lin's estimate of floor(V / p) for V = pa - na, from the signed per-limb
+    sums of limbs 10 and 11 in double precision (exactly the device's operations); it is within 1
+    of floor(V / p), so V - (q - 1) p lies in [0, 3p)."""
+    def limb_sum(v, j):
+        return sum(c * ((x >> (32 * j)) & 0xFFFFFFFF) for c, x in v)
+    d11 = limb_sum(pa, 11) - limb_sum(na, 11)
+    d10 = limb_sum(pa, 10) - limb_sum(na, 10)
+    w = float(d11) * 4294967296.0 + float(d10)
+    return math.floor(w * INV_P320)
+
+
 def run_encoded(code, slots):
-    """Interpret an encoded program over a dict slot -> int (mod P), the way lb_wave.h does:
-    lazy positive / negated sums and the per-phase reduction bound are checked too."""
+    """Interpret an encoded program over a dict slot -> int, the way lb_wave.h does: products
+    are reduced below p, linear combinations V = pos - neg are reduced to V - (q - 1) p in
+    [0, 3p) by the quotient estimate (program outputs: fully below p), and slots keep those
+    unreduced representatives, whose limbs feed the next estimates."""
     n_ph, n_temp, n_out = code[0], code[1], code[2]
     outs = code[3:3 + n_out]
     pos = 3 + n_out
     pos += -pos % 8
     S = dict(slots)
 
-    def lin(rec, off, np_, nn_, red_):
-        bound, m = red_ & 0xFF, red_ >> 8
-        pa = sum(rec[off + 2 * k + 1] * S[rec[off + 2 * k]] for k in range(np_))
-        na = sum(rec[off + 2 * k + 1] * S[rec[off + 2 * k]] for k in range(np_, np_ + nn_))
-        r = pa + ((1 << (m - 1)) * P if m else 0) - na
-        assert 0 <= r < bound * P, "lazy reduction bound"
-        for j in range(6, -1, -1):
-            if (1 << j) < bound and r >= (1 << j) * P:
-                r -= (1 << j) * P
-        assert r < P
+    def lin(rec, off, np_, nn_, full=False):
+        pa = [(rec[off + 2 * k + 1], S[rec[off + 2 * k]]) for k in range(np_)]
+        na = [(rec[off + 2 * k + 1], S[rec[off + 2 * k]]) for k in range(np_, np_ + nn_)]
+        v = sum(c * x for c, x in pa) - sum(c * x for c, x in na)
+        r = v - (quotient_estimate(pa, na) - 1) * P
+        assert 0 <= r < 3 * P, "quotient estimate"
+        if full:
+            r %= P
         return r
 
     for _ in range(n_ph):
@@ -422,11 +439,13 @@ def run_encoded(code, slots):
         for k in range(n):
             rec = code[pos + k * rs: pos + (k + 1) * rs]
             if kind == 0:
-                new[rec[0]] = lin(rec, 1, npa, nna, ra) * lin(rec, 1 + 2 * MAXP, npb, nnb, rb) % P
+                new[rec[0]] = lin(rec, 1, npa, nna) * lin(rec, 1 + 2 * MAXP, npb, nnb) % P
             else:
-                new[rec[0]] = lin(rec, 1, npa, nna, ra)
+                new[rec[0] & ~OUT_FLAG] = lin(rec, 1, npa, nna, full=bool(rec[0] & OUT_FLAG))
         S.update(new)
         pos += n * rs
+    for o in outs:
+        assert 0 <= S[o] < P, "program outputs are reduced"
     return [S[o] for o in outs]
 
 
@@ -490,7 +509,11 @@ def _ref_checks(progs, codes):
     assert o.final_exponentiation(ml) == e, "Miller step programs"
 
 
-def main():
+OUT_PATH = os.path.join(ROOT, "lodestar_amd", "csrc", "lb_wave_progs.h")
+
+
+def render():
+    """Build, encode and check every program; return (programs, codes, header text)."""
     progs = build_programs()
     codes = {k: v.encode() for k, v in progs.items()}
     _ref_checks(progs, codes)
@@ -502,20 +525,36 @@ def main():
              f"#define LBW_LREC {LREC}",
              f"#define LBW_IN {IN_BASE}", f"#define LBW_CONST {CONST_BASE}", f"#define LBW_TEMP {TEMP_BASE}",
              f"#define LBW_C_B3 {C_B3}", f"#define LBW_C_INV2 {C_INV2}", f"#define LBW_C_FROB1 {C_FROB1}",
-             f"#define LBW_C_FROB2 {C_FROB2}", f"#define LBW_C_ZERO {C_ZERO}", f"#define LBW_N_CONST {N_CONST}"]
-    maxtemp = 0
-    for name, code in codes.items():
-        pg = progs[name]
+             f"#define LBW_C_FROB2 {C_FROB2}", f"#define LBW_C_ZERO {C_ZERO}", f"#define LBW_N_CONST {N_CONST}",
+             f"#define LBW_OUT_FLAG {OUT_FLAG:#x}",
+             f"#define LBW_INV_P320 {INV_P320.hex()}  // 2^320 / p, nearest double"]
+    # one image, programs at 16-byte aligned offsets; kernels copy a prefix of it into LDS
+    # (LBW_PROGS_FE: the Fp12 programs; LBW_PROGS_ALL: + the Miller steps)
+    order = ["MUL12", "SQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP"]
+    assert sorted(order) == sorted(codes)
+    maxtemp, image = 0, []
+    for name in order:
+        code, pg = codes[name], progs[name]
+        assert len(code) % 8 == 0
         maxtemp = max(maxtemp, pg.ntemp)
-        nph = code[0]
-        lines.append(f"// {name}: {len(pg.prods)} products, {len(pg.lins)} linear tasks, {nph} phases, "
-                     f"{pg.ntemp} temps")
-        body = ", ".join(str(v) for v in code)
-        lines.append(f"static __device__ const int16_t __attribute__((aligned(16))) LBW_{name}[{len(code)}] = {{{body}}};")
+        lines.append(f"// {name}: {len(pg.prods)} products, {len(pg.lins)} linear tasks, {code[0]} phases, "
+                     f"{pg.ntemp} temps, offset {len(image)}")
+        lines.append(f"#define LBW_{name} {len(image)}")
+        image += code
+        if name == "FROB2":
+            lines.append(f"#define LBW_PROGS_FE {len(image)}")
+    lines.append(f"#define LBW_PROGS_ALL {len(image)}")
+    body = ", ".join(str(v) for v in image)
+    lines.append(f"static __device__ const int16_t __attribute__((aligned(16))) LBW_PROGS[{len(image)}] = {{{body}}};")
     lines.append(f"#define LBW_MAX_TEMPS {maxtemp}")
-    out = os.path.join(ROOT, "lodestar_amd", "csrc", "lb_wave_progs.h")
+    return progs, codes, "\n".join(lines) + "\n"
+
+
+def main():
+    progs, codes, text = render()
+    out = OUT_PATH
     with open(out, "w") as fh:
-        fh.write("\n".join(lines) + "\n")
+        fh.write(text)
     for name, pg in progs.items():
         print(f"{name}: {len(pg.prods)} products, {len(pg.lins)} lins, {codes[name][0]} phases, {pg.ntemp} temps")
     print("wrote", out)

@@ -18,13 +18,13 @@ __global__ void __launch_bounds__(64) k_lin(long long* out, const int16_t* rec_g
   fp acc = fp_zero();
   long long t0 = clock64();
   for (int it = 0; it < 8; it++) {
-    fp r = w_lin<LBW_MAXL>(S, rec + 1, 12, 12, 32 | (6 << 8));
+    fp r = w_lin<LBW_MAXL>(S, rec + 1, 12, 12, false);
     acc.v[it % 12] ^= r.v[0];
     rec[1] ^= (int16_t)(r.v[1] & 1);
   }
   long long t1 = clock64();
   for (int it = 0; it < 8; it++) {
-    fp r = w_lin<LBW_MAXP>(S, rec + 1, 8, 0, 8);
+    fp r = w_lin<LBW_MAXP>(S, rec + 1, 8, 0, false);
     acc.v[it % 12] ^= r.v[0];
     rec[1] ^= (int16_t)(r.v[1] & 1);
   }
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(64) k_lin(long long* out, const int16_t* rec_g
   uint32_t r13[13];
   for (int j = 0; j < 13; j++) r13[j] = (uint32_t)pa[j % 12];
   for (int it = 0; it < 8; it++) {
-    LB_UNROLL for (int j = 6; j >= 0; j--) w_csub13(r13, w_pmul(j));
+    LB_UNROLL for (int j = 6; j >= 0; j--) w_csub13(r13, j ? LB_P_X2 : LB_P_X1);
     r13[0] ^= it;
   }
   long long t5 = clock64();

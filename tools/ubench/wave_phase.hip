@@ -6,9 +6,9 @@
 #include "lb_kernels.h"
 
 __global__ void __launch_bounds__(64) k_phase(long long* out) {
-  LBW_SHARED(S);
+  LBW_SHARED_ML(S);
   const int lane = threadIdx.x;
-  w_init_consts(S);
+  w_init_consts(S, LBW_PROGS_ALL);
   if (lane < 12) { fp v = fp_one(); v.v[0] += lane; w_st(S, LBW_A(0) + lane, v); w_st(S, LBW_A(1) + lane, v); }
   if (lane < 24) { fp v = fp_one(); v.v[1] += lane; w_st(S, LBW_IN + lane, v); }
   w_sync();
@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(64) k_phase(long long* out) {
   w_in(S, 24, lane < 12 ? LBW_A(0) + lane : LBW_A(1) + (lane - 12));
   q1 = clock64();
   {
-    const int16_t* prog = LBW_MUL12;
+    const lds_i16* prog = w_progs(S) + LBW_MUL12;
     const int nph = prog[0], nout = prog[2];
     int pos = 3 + nout;
     pos += (-pos) & 7;
@@ -50,8 +50,8 @@ __global__ void __launch_bounds__(64) k_phase(long long* out) {
           int16_t rec[LBW_PREC];
           w_fetch<LBW_PREC>(rec, prog + pos + k * LBW_PREC);
           f1 = clock64();
-          fp x = w_lin<LBW_MAXP>((lds_fp*)S, rec + 1, npa, nna, ra);
-          fp y = w_lin<LBW_MAXP>((lds_fp*)S, rec + 1 + 2 * LBW_MAXP, npb, nnb, rb);
+          fp x = w_lin<LBW_MAXP>((lds_fp*)S, rec + 1, npa, nna, false);
+          fp y = w_lin<LBW_MAXP>((lds_fp*)S, rec + 1 + 2 * LBW_MAXP, npb, nnb, false);
           f2 = clock64();
           w_st(S, rec[0], fp_mul(x, y));
         }
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(64) k_phase(long long* out) {
           int16_t rec[LBW_LREC];
           w_fetch<LBW_LREC>(rec, prog + pos + k * LBW_LREC);
           f1 = clock64();
-          w_st(S, rec[0], w_lin<LBW_MAXL>((lds_fp*)S, rec + 1, npa, nna, ra));
+          w_st(S, rec[0] & ~LBW_OUT_FLAG, w_lin<LBW_MAXL>((lds_fp*)S, rec + 1, npa, nna, (rec[0] & LBW_OUT_FLAG) != 0));
           f2 = clock64();
         }
         pos += n * LBW_LREC;
