@@ -23,10 +23,13 @@ then per phase a header [kind, n_tasks, npA, nnA, npB, nnB, redA, redB] + fixed-
 (PREC / LREC entries, 16-byte multiples, so a lane fetches its record with 16-byte vector
 loads); kind 0 = product phase, record [dst, (slot, coef) * MAXP for x, (slot, coef) * MAXP for
 y]; kind 1 = linear phase, record [dst, (slot, coef) * MAXL] (operand A only).  Within an
-operand the positive terms come first, padded to the phase-uniform count npA, then the negated
-ones (coefficients stored as magnitudes), padded to nnA; padding pairs have coefficient 0.  So every lane of a phase runs the same term loop with no sign branches.  red = B | (m << 8):
-the lazy sum is r = sum(pos) + 2^(m-1) p - sum(neg) < B p (m = 0: no negated terms), reduced
-by conditional subtraction of 2^j p for every 2^j < B.
+operand the positive terms come first (phase-uniform count npA), the negated ones (coefficients
+stored as magnitudes) fill the last nnA pairs, and padding pairs have coefficient 0.  So every
+lane of a phase runs the same term loop with no sign branches.  redA / redB = B | (m << 8)
+record the phase's bound on sum(pos) + 2^(m-1) p - sum(neg) in units of p (B <= 128, checked
+here; the device no longer reads them: lb_wave.h w_lin reduces by a quotient estimate, which
+run_encoded below mirrors).  A linear task whose dst carries OUT_FLAG is a program output and
+is reduced below p; every other temp is left in [0, 3p).
 
 The program encoding is validated here by a Python interpreter against direct big-integer
 evaluation of the same tower formulas (and, through the engine tests, against the oracle).
@@ -167,14 +170,15 @@ class Prog:
             return bound | (m << 8)
 
         def pack(ops, np_, nn_, width):
-            rec = []
-            for p, n in [ops]:
-                for k in range(np_):
-                    rec += list(p[k]) if k < len(p) else pad
-                for k in range(nn_):
-                    rec += list(n[k]) if k < len(n) else pad
+            # positive pairs from the front, negated pairs at the back: [width - nn_, width)
+            p, n = ops
             assert np_ + nn_ <= width
-            return rec + pad * (width - np_ - nn_)
+            rec = []
+            for k in range(width - nn_):
+                rec += list(p[k]) if k < len(p) else pad
+            for k in range(nn_):
+                rec += list(n[k]) if k < len(n) else pad
+            return rec
 
         for kind, tasks in phases:
             if kind == 0:
@@ -421,9 +425,9 @@ def run_encoded(code, slots):
     pos += -pos % 8
     S = dict(slots)
 
-    def lin(rec, off, np_, nn_, full=False):
+    def lin(rec, off, np_, nn_, width, full=False):
         pa = [(rec[off + 2 * k + 1], S[rec[off + 2 * k]]) for k in range(np_)]
-        na = [(rec[off + 2 * k + 1], S[rec[off + 2 * k]]) for k in range(np_, np_ + nn_)]
+        na = [(rec[off + 2 * k + 1], S[rec[off + 2 * k]]) for k in range(width - nn_, width)]
         v = sum(c * x for c, x in pa) - sum(c * x for c, x in na)
         r = v - (quotient_estimate(pa, na) - 1) * P
         assert 0 <= r < 3 * P, "quotient estimate"
@@ -439,9 +443,9 @@ def run_encoded(code, slots):
         for k in range(n):
             rec = code[pos + k * rs: pos + (k + 1) * rs]
             if kind == 0:
-                new[rec[0]] = lin(rec, 1, npa, nna) * lin(rec, 1 + 2 * MAXP, npb, nnb) % P
+                new[rec[0]] = lin(rec, 1, npa, nna, MAXP) * lin(rec, 1 + 2 * MAXP, npb, nnb, MAXP) % P
             else:
-                new[rec[0] & ~OUT_FLAG] = lin(rec, 1, npa, nna, full=bool(rec[0] & OUT_FLAG))
+                new[rec[0] & ~OUT_FLAG] = lin(rec, 1, npa, nna, MAXL, full=bool(rec[0] & OUT_FLAG))
         S.update(new)
         pos += n * rs
     for o in outs:
