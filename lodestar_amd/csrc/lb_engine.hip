@@ -661,7 +661,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(LB_MSM_NB)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
                          e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB);
-      hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(1), dim3(16 * LB_MSM_W), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
+      hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(1), dim3(64 * LB_MSM_W), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
                          e->treeS.as<uint32_t>(), 2 * mj, 1u);
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
@@ -907,7 +907,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
-      hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(16 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
+      hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(64 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
                          U(SX_S), cm, 0u);
     }
     if (c)

@@ -664,42 +664,53 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t*
   soa_st(bsum, nb, b, acc);
 }
 // One workgroup per MSM instance j of W windows (buckets [j W 256, (j+1) W 256) of bsum, stride
-// nb): lane (w, s) owns digits [16 s, 16 s + 16) of window w.  Running sums give
-// Y = sum_j j B_{16s+j} and T = sum_j B_{16s+j}; Y + 16 s T is the segment's share of
-// sum_d d B_d.  Segments then add up in an LDS tree, and the windows combine Horner-style:
-// S = sum_w 2^(8w) W_w  -> element out0 + j of `out` (SoA, stride n_out).  W = 4 (32-bit
-// scalars) for the batch MSM, 5 for the search's weighted scalars (up to 40 bits).
+// nb), one wave per window: lane s owns digits [4 s, 4 s + 4).  A lane's running sums give
+// Y_s = sum_j j B_{4s+j} and T_s = sum_j B_{4s+j} (5 additions); then
+//   sum_d d B_d = sum_s (Y_s + 4 s T_s) = sum_s Y_s + 4 sum_{k >= 1} U_k,  U_k = sum_{s >= k} T_s,
+// so a suffix scan of T across the wave (6 levels of shuffles + additions), V_s = Y_s + 4 U_s
+// (s >= 1; two doublings) and a shuffle tree over V (6 levels) give the window sum W_w in lane 0.
+// Lane 0 of wave 0 combines the windows Horner-style: S = sum_w 2^(8w) W_w -> element out0 + j of
+// `out` (SoA, stride n_out).  The dependent chain is ~19 additions + 2 doublings + the Horner
+// doublings, against 34 additions + 12 doublings + the Horner for 16 lanes of 16 digits.  W = 4
+// (32-bit scalars) for the batch MSM, 5 for the search's weighted scalars (up to 40 bits).
+__device__ __forceinline__ g2j g2j_shfl_down(const g2j& a, unsigned d) {
+  return g2j{fp2{fp_shfl_down(a.x.c0, d), fp_shfl_down(a.x.c1, d)},
+             fp2{fp_shfl_down(a.y.c0, d), fp_shfl_down(a.y.c1, d)},
+             fp2{fp_shfl_down(a.z.c0, d), fp_shfl_down(a.z.c1, d)}};
+}
 template <int W>
-__global__ void __launch_bounds__(16 * W) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
+__global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
                                                        uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
-  static_assert(LB_MSM_B == 256, "16 lanes of 16 digits per window");
-  __shared__ g2j sh[16 * W];
-  const uint32_t lane = threadIdx.x, w = lane >> 4, sg = lane & 15u, base = blockIdx.x * (W * LB_MSM_B);
-  g2j run = jac_infinity<fp2>(), y = jac_infinity<fp2>();
-  for (int j = 15; j >= 1; j--) {
-    run = jac_add_i(run, soa_ld<g2j>(bsum, nb, base + w * LB_MSM_B + 16 * sg + j));
-    y = jac_add_i(y, run);
+  static_assert(LB_MSM_B == 256, "64 lanes of 4 digits per window");
+  __shared__ g2j win[W];
+  const uint32_t s = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t* bw = bsum;  // bucket (instance, w, d) at element blockIdx.x * W * 256 + w * 256 + d
+  const uint32_t e0 = blockIdx.x * (W * LB_MSM_B) + w * LB_MSM_B + 4 * s;
+  g2j run = soa_ld<g2j>(bw, nb, e0 + 3);
+  g2j y = run;
+  run = jac_add_i(run, soa_ld<g2j>(bw, nb, e0 + 2));
+  y = jac_add_i(y, run);
+  run = jac_add_i(run, soa_ld<g2j>(bw, nb, e0 + 1));
+  y = jac_add_i(y, run);  // 3 B3 + 2 B2 + B1
+  g2j u = s ? jac_add_i(run, soa_ld<g2j>(bw, nb, e0)) : run;  // digit 0 is unused
+  // inclusive suffix scan: u_s = sum_{t >= s} T_t
+  LB_UNROLL for (unsigned d = 1; d < 64; d <<= 1) {
+    const g2j o = g2j_shfl_down(u, d);
+    if (s + d < 64) u = jac_add_i(u, o);
   }
-  if (sg) run = jac_add_i(run, soa_ld<g2j>(bsum, nb, base + w * LB_MSM_B + 16 * sg));
-  // y += 16 sg * run   (sg < 16: 4-bit double-and-add, then 4 doublings)
-  g2j t = jac_infinity<fp2>();
-  for (int b = 3; b >= 0; b--) {
-    t = jac_dbl_i(t);
-    if ((sg >> b) & 1u) t = jac_add_i(t, run);
+  g2j v = y;
+  if (s) v = jac_add_i(v, jac_dbl_i(jac_dbl_i(u)));
+  LB_UNROLL for (unsigned d = 32; d >= 1; d >>= 1) {
+    const g2j o = g2j_shfl_down(v, d);
+    if (s < d) v = jac_add_i(v, o);
   }
-  for (int b = 0; b < 4; b++) t = jac_dbl_i(t);
-  y = jac_add_i(y, t);
-  sh[lane] = y;
+  if (s == 0) win[w] = v;
   __syncthreads();
-  for (uint32_t d = 8; d >= 1; d >>= 1) {
-    if (sg < d) sh[lane] = jac_add_i(sh[lane], sh[lane + d]);
-    __syncthreads();
-  }
-  if (lane == 0) {
-    g2j S = sh[16 * (W - 1)];
+  if (threadIdx.x == 0) {
+    g2j S = win[W - 1];
     for (int ww = W - 2; ww >= 0; ww--) {
       for (int b = 0; b < LB_MSM_C; b++) S = jac_dbl_i(S);
-      S = jac_add_i(S, sh[16 * ww]);
+      S = jac_add_i(S, win[ww]);
     }
     soa_st(out, n_out, out0 + blockIdx.x, S);
   }
