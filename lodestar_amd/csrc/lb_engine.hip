@@ -119,6 +119,8 @@ struct lb_engine {
   // batches with at most this many distinct roots run their Miller loops one wave per root
   // (k_miller_wave); larger ones one lane per root (k_miller_grouped).  LB_MILLER_WAVE_MAX.
   uint32_t miller_wave_max = 2048;
+  // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
+  uint32_t hash_g8_max = 2048;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -239,6 +241,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
+  if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -640,8 +643,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_HASH_FIN, s1);
-      hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
-                         e->h_aff.as<uint32_t>());
+      if (nuh <= e->hash_g8_max)
+        hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
+                           e->h_aff.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
+                           e->h_aff.as<uint32_t>());
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
     {

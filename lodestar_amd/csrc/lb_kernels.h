@@ -81,6 +81,7 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 #include "lb_wave.h"
+#include "lb_group.h"
 #include "lb_ssz.h"
 
 // ---------------------------------------------------------------- block-wide batch inversion
@@ -257,6 +258,37 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n,
     a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
   }
   soa_st(h_aff, n, i, a);
+}
+
+// The same with 8 lanes per root (lb_group.h: each G2 doubling in 3 levels of Fp products, each
+// addition in 6), for batches with few distinct roots, where k_hash_finish's lone-lane
+// cofactor clearing (~2 700 serial Fp products) is the longest step of the per-root chain.
+// Blocks of 64 threads = 8 roots; idle groups of the last block recompute the last root.
+__global__ void __launch_bounds__(64) k_hash_finish_g8(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                       const uint32_t* __restrict__ q, uint32_t* __restrict__ h_aff) {
+  const uint32_t nu = *n_u;
+  if (blockIdx.x * 8 >= nu) return;  // whole block idle (uniform: fp_inv_block is safe)
+  const uint32_t u = blockIdx.x * 8 + (threadIdx.x >> 3);
+  const bool act = u < nu;
+  const uint32_t uc = act ? u : nu - 1;
+  g2j h = soa_ld<g2j>(q, 2 * n, uc);
+  g8_add(h, soa_ld<g2j>(q, 2 * n, n + uc));
+  h = g8_clear_cofactor(h);
+  const fp nz = fp_add(fp_sqr(h.z.c0), fp_sqr(h.z.c1));
+  const bool zero = fp_is_zero(nz);
+  const fp ni = fp_inv_block(zero ? fp_one() : nz);
+  if (!act || g8_q() != 0) return;
+  g2a a;
+  if (zero) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    const fp2 zi{fp_mul(h.z.c0, ni), fp_neg(fp_mul(h.z.c1, ni))};
+    const fp2 zi2 = fp2_sqr(zi);
+    a.x = fp2_mul(h.x, zi2);
+    a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
+  }
+  soa_st(h_aff, n, u, a);
 }
 
 // ---------------------------------------------------------------- pubkeys + blinding

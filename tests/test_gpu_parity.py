@@ -561,3 +561,31 @@ def test_direct_verify_callers(engine):
         assert pool.aggregate_signatures(sigs).hex() == load_json("aggregates.json")["signature_aggregate"][2]["expected96"]
     finally:
         asyncio.run(pool.close())
+
+
+@pytest.mark.parametrize("name", ["c3_mixed", "c2"])
+def test_per_root_kernel_forms_agree(monkeypatch, name):
+    """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
+    lane per root (k_hash_finish, k_miller_grouped) and many lanes per root (k_hash_finish_g8:
+    8-lane G2 doublings / additions; k_miller_wave: the wave engine).  Engines created with the
+    thresholds at 0 and at 2^31 run the same batch (same blinding scalars) through each form;
+    verdicts must match the planted expectation, and the root partials (576-byte Fp12 products
+    before the final exponentiation) must be byte-identical."""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    outs = []
+    for lim in ("0", str(1 << 31)):
+        monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
+        monkeypatch.setenv("LB_HASH_G8_MAX", lim)
+        with Engine(0) as e:
+            wl = W.make(e, name)
+            b = e.upload(W.indexed_for(e, wl))
+            try:
+                sc = np.random.default_rng(5).integers(1, 1 << 63, size=wl.packed.n_sets, dtype=np.uint64)
+                got = np.asarray(b.verify(scalars=sc))[:wl.packed.n_jobs]
+                part = bytes(b.partial(scalars=sc)[0]) if (wl.expected == 1).all() else None
+            finally:
+                b.free()
+        assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
+        outs.append(part)
+    assert outs[0] == outs[1]
