@@ -180,6 +180,34 @@ int32_t lb_merkleize(lb_engine* e, uint32_t n_trees, const uint32_t* chunk_offse
                      const uint32_t* depths, const uint64_t* mix_lengths, uint8_t* out_roots32);
 
 /*
+ * KZG (EIP-4844 blobs; the c-kzg calls behind packages/beacon-node/src/util/kzg.ts:15-65, SURVEY.md
+ * §8(f) row 4).  The host side (lodestar_amd/kzg.py) does the scalar-field work; these do the group
+ * work on the GPU.
+ *
+ * lb_kzg_load_setup (ckzg.loadTrustedSetup, kzg.ts:54-67): the monomial-form setup as Lodestar's
+ * trusted_setup.bin holds it -- n_g1 compressed [tau^i] G1 (48 B each) and at least two compressed
+ * [tau^i] G2 (96 B each; [tau^0] G2 and [tau^1] G2 are kept).  Every point is decoded and checked
+ * (curve, subgroup); out_status[i] per G1 point, and LB_POINT_NOT_IN_GROUP is returned for a bad
+ * G2 point.  Replaces any previously loaded setup of this engine.
+ */
+int32_t lb_kzg_load_setup(lb_engine* e, const uint8_t* g1_48, uint32_t n_g1, const uint8_t* g2_96, uint32_t n_g2,
+                          int32_t* out_status);
+
+/*
+ * G1 linear combination out48 = compress(sum_i s_i P_i) (the spec's g1_lincomb): P_i = setup point i
+ * (points48 == NULL; n <= the loaded setup size), or n compressed points (points48).  scalars32:
+ * n little-endian 32-byte scalars below r.  Returns the decode error of the first bad point.
+ */
+int32_t lb_g1_lincomb(lb_engine* e, uint32_t n, const uint8_t* points48, const uint8_t* scalars32, uint8_t* out48);
+
+/*
+ * verify_kzg_proof_impl: *ok = 1 iff e(C - [y] G1, -G2) e(proof, [tau] G2 - [z] G2) == 1, else 0;
+ * *ok = -code if C or proof fails to decode.  z32, y32: little-endian scalars below r.
+ */
+int32_t lb_kzg_verify_proof(lb_engine* e, const uint8_t* commitment48, const uint8_t* z32, const uint8_t* y32,
+                            const uint8_t* proof48, int32_t* ok);
+
+/*
  * Synthetic-data helpers for tests and the benchmark (not on the verification path):
  * SecretKey.toPublicKey and SecretKey.sign as used by the reference's own tests
  * (test/e2e/chain/bls/multithread.test.ts:28-31).  Secret keys are 32-byte big-endian < r.

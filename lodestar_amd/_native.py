@@ -64,6 +64,9 @@ SIGNATURES = {
                                                  _i32p]),
     "lb_g1_decompress": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _i32p, ctypes.c_int32]),
     "lb_merkleize": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u8p, _u32p, _u64p, _u8p]),
+    "lb_kzg_load_setup": (ctypes.c_int32, [_vp, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, _i32p]),
+    "lb_g1_lincomb": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),
+    "lb_kzg_verify_proof": (ctypes.c_int32, [_vp, _u8p, _u8p, _u8p, _u8p, _i32p]),
     "lb_sk_to_pk": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),
     "lb_sign": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, _u8p, _u8p]),
     "lb_pubkey_table_append": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_int32, _i32p,

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "lb_kernels.h"
+#include "lb_kzg.h"
 
 #define LB_ABI_VERSION 1
 
@@ -121,10 +122,15 @@ struct lb_engine {
   uint32_t miller_wave_max = 2048;
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
+  // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
+  uint32_t subgroup_g8_max = 4096;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
   uint32_t table_n = 0, table_cap = 0;
+  // KZG trusted setup (lb_kzg_load_setup): [tau^i] G1 as g1a SoA (kzg_n entries), [tau^0,1] G2
+  dbuf kzg_g1, kzg_g2;
+  uint32_t kzg_n = 0;
   // profiling
   bool profiling = false;
   hipEvent_t ev0[kStages] = {}, ev1[kStages] = {};
@@ -242,6 +248,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
+  if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -603,8 +610,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
                          b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
-      hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
-                         e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      if (n <= e->subgroup_g8_max)
+        hipLaunchKernelGGL(k_sig_subgroup_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      else
+        hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
       hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s2, nj, b->d_job_off.as<uint32_t>(),
                          e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
                          e->set_live.as<uint32_t>());
@@ -1429,5 +1440,98 @@ extern "C" int32_t lb_sign(lb_engine* e, uint32_t n, const uint8_t* sks32, const
                     [&](std::vector<void*>& p) {
                       hipLaunchKernelGGL(k_sign, dim3(nblk(n)), dim3(LB_TPB), 0, e->stream, n,
                                          (const uint8_t*)p[0], (const uint8_t*)p[1], (uint8_t*)p[2]);
+                    });
+}
+
+// ---------------------------------------------------------------- KZG (lb_kzg.h)
+extern "C" int32_t lb_kzg_load_setup(lb_engine* e, const uint8_t* g1_48, uint32_t n_g1, const uint8_t* g2_96,
+                                     uint32_t n_g2, int32_t* out_status) {
+  if (!e || !n_g1 || !g1_48 || !g2_96 || n_g2 < 2 || !out_status) return LB_ERR_ARGUMENT;
+  std::vector<int32_t> st2(2, LB_OK);
+  int32_t r;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    LB_HIP(hipSetDevice(e->device));
+    LB_HIP(e->kzg_g1.ensure((size_t)n_g1 * sizeof(g1a)));
+    LB_HIP(e->kzg_g2.ensure(2 * sizeof(g2a)));
+  }
+  lb_engine* ee = e;
+  r = run_simple(e, {{g1_48, (size_t)n_g1 * 48, false, nullptr}, {nullptr, (size_t)n_g1 * 4, true, out_status},
+                     {g2_96, 2 * 96, false, nullptr}, {nullptr, 2 * 4, true, st2.data()}},
+                 [&](std::vector<void*>& p) {
+                   hipLaunchKernelGGL(k_kzg_setup_g1, dim3(nblk(n_g1)), dim3(LB_TPB), 0, ee->stream, n_g1,
+                                      (const uint8_t*)p[0], ee->kzg_g1.as<uint32_t>(), n_g1, (int32_t*)p[1]);
+                   hipLaunchKernelGGL(k_kzg_setup_g2, dim3(1), dim3(64), 0, ee->stream, (const uint8_t*)p[2],
+                                      ee->kzg_g2.as<uint32_t>(), (int32_t*)p[3]);
+                 });
+  if (r != LB_OK) return r;
+  if (st2[0] != LB_OK || st2[1] != LB_OK) {
+    e->kzg_n = 0;
+    return st2[0] != LB_OK ? st2[0] : st2[1];
+  }
+  for (uint32_t i = 0; i < n_g1; i++)
+    if (out_status[i] != LB_OK) {
+      e->kzg_n = 0;
+      return out_status[i];
+    }
+  e->kzg_n = n_g1;
+  return LB_OK;
+}
+
+extern "C" int32_t lb_g1_lincomb(lb_engine* e, uint32_t n, const uint8_t* points48, const uint8_t* scalars32,
+                                 uint8_t* out48) {
+  if (!e || !out48 || (n && !scalars32)) return LB_ERR_ARGUMENT;
+  if (!points48 && n > e->kzg_n) return LB_ERR_ARGUMENT;
+  if (!n) {  // empty sum: infinity
+    memset(out48, 0, 48);
+    out48[0] = 0xc0;
+    return LB_OK;
+  }
+  uint32_t levels = 0;
+  for (uint32_t m = n; m > 1; m = (m + 63) / 64) levels++;
+  const uint32_t n1 = (n + 63) / 64;
+  std::vector<int32_t> st(n, LB_OK);
+  lb_engine* ee = e;
+  const int32_t r = run_simple(
+      e, {{points48, points48 ? (size_t)n * 48 : 0, false, nullptr}, {scalars32, (size_t)n * 32, false, nullptr},
+          {nullptr, (size_t)n * sizeof(g1j), true, nullptr}, {nullptr, (size_t)n1 * sizeof(g1j), true, nullptr},
+          {nullptr, (size_t)n * 4, true, st.data()}, {nullptr, 48, true, out48}},
+      [&](std::vector<void*>& p) {
+        hipLaunchKernelGGL(k_g1_terms, dim3(nblk(n)), dim3(LB_TPB), 0, ee->stream, n,
+                           points48 ? (const uint8_t*)p[0] : nullptr, ee->kzg_g1.as<uint32_t>(), ee->kzg_n,
+                           (const uint32_t*)p[1], (uint32_t*)p[2], (int32_t*)p[4]);
+        // reduce 64:1 per level, ping-ponging between the term buffer and the partials buffer
+        uint32_t* bufs[2] = {(uint32_t*)p[2], (uint32_t*)p[3]};
+        uint32_t m = n;
+        int cur = 0;
+        for (uint32_t l = 0; l < levels; l++) {
+          const uint32_t mo = (m + 63) / 64;
+          hipLaunchKernelGGL(k_g1_sum64, dim3(mo), dim3(64), 0, ee->stream, m, bufs[cur], mo, bufs[cur ^ 1]);
+          m = mo;
+          cur ^= 1;
+        }
+        hipLaunchKernelGGL(k_g1_out48, dim3(1), dim3(64), 0, ee->stream, bufs[cur], m, (uint8_t*)p[5]);
+      });
+  if (r != LB_OK) return r;
+  for (uint32_t i = 0; i < n; i++)
+    if (st[i] != LB_OK) return st[i];
+  return LB_OK;
+}
+
+extern "C" int32_t lb_kzg_verify_proof(lb_engine* e, const uint8_t* commitment48, const uint8_t* z32,
+                                       const uint8_t* y32, const uint8_t* proof48, int32_t* ok) {
+  if (!e || !commitment48 || !z32 || !y32 || !proof48 || !ok) return LB_ERR_ARGUMENT;
+  if (e->kzg_n == 0) return LB_ERR_ARGUMENT;  // no setup loaded
+  uint8_t io[96];
+  memcpy(io, commitment48, 48);
+  memcpy(io + 48, proof48, 48);
+  uint8_t yz[64];
+  memcpy(yz, y32, 32);
+  memcpy(yz + 32, z32, 32);
+  lb_engine* ee = e;
+  return run_simple(e, {{io, 96, false, nullptr}, {yz, 64, false, nullptr}, {nullptr, 4, true, ok}},
+                    [&](std::vector<void*>& p) {
+                      hipLaunchKernelGGL(k_kzg_check, dim3(1), dim3(64), 0, ee->stream, (const uint8_t*)p[0],
+                                         (const uint32_t*)p[1], ee->kzg_g2.as<uint32_t>(), (int32_t*)p[2]);
                     });
 }

@@ -206,6 +206,21 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n
   if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
 }
 
+// The same test with 8 lanes per signature (lb_group.h), for small batches (a 1-set call, a
+// block): the |x| ladder's 63 doublings take 3 product levels each instead of 16 serial products.
+__global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                        const uint32_t* __restrict__ sig_inf,
+                                                        int32_t* __restrict__ sig_status) {
+  const uint32_t i = blockIdx.x * 8 + (threadIdx.x >> 3);
+  if (i >= n) return;  // uniform within the group
+  if (sig_status[i] != LB_OK || sig_inf[i]) return;
+  const g2j p = jac_from_aff(soa_ld<g2a>(sig_aff, n, i));
+  const g2j acc = g8_mul_xabs(p);
+  bool ok = !jac_is_inf(acc);  // psi(P) is finite
+  if (ok) ok = jac_eq(g8_psi(p), jac_neg(acc));
+  if (!ok && g8_q() == 0) sig_status[i] = LB_POINT_NOT_IN_GROUP;
+}
+
 // ---------------------------------------------------------------- hash_to_G2
 // Hashing runs once per DISTINCT signing root (k_msg_insert below): launched over 2 nu threads
 // (nu = distinct roots, read back by the host); thread t handles unique message t % nu, field
@@ -726,13 +741,15 @@ __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restric
   y = jac_add_i(y, run);  // 3 B3 + 2 B2 + B1
   g2j u = s ? jac_add_i(run, soa_ld<g2j>(bw, nb, e0)) : run;  // digit 0 is unused
   // inclusive suffix scan: u_s = sum_{t >= s} T_t
-  LB_UNROLL for (unsigned d = 1; d < 64; d <<= 1) {
+  for (int l = 0; l < 6; l++) {  // rolled: the body is an inlined G2 addition
+    const unsigned d = 1u << l;
     const g2j o = g2j_shfl_down(u, d);
     if (s + d < 64) u = jac_add_i(u, o);
   }
   g2j v = y;
   if (s) v = jac_add_i(v, jac_dbl_i(jac_dbl_i(u)));
-  LB_UNROLL for (unsigned d = 32; d >= 1; d >>= 1) {
+  for (int l = 5; l >= 0; l--) {
+    const unsigned d = 1u << l;
     const g2j o = g2j_shfl_down(v, d);
     if (s < d) v = jac_add_i(v, o);
   }

@@ -567,7 +567,8 @@ def test_direct_verify_callers(engine):
 def test_per_root_kernel_forms_agree(monkeypatch, name):
     """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
     lane per root (k_hash_finish, k_miller_grouped) and many lanes per root (k_hash_finish_g8:
-    8-lane G2 doublings / additions; k_miller_wave: the wave engine).  Engines created with the
+    8-lane G2 doublings / additions; k_miller_wave: the wave engine); likewise the signatures'
+    subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count).  Engines created with the
     thresholds at 0 and at 2^31 run the same batch (same blinding scalars) through each form;
     verdicts must match the planted expectation, and the root partials (576-byte Fp12 products
     before the final exponentiation) must be byte-identical."""
@@ -577,6 +578,7 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     for lim in ("0", str(1 << 31)):
         monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
+        monkeypatch.setenv("LB_SUBGROUP_G8_MAX", lim)
         with Engine(0) as e:
             wl = W.make(e, name)
             b = e.upload(W.indexed_for(e, wl))
