@@ -260,6 +260,16 @@ def extra_legs(a, engs, barrier, W):
                      "sets_per_s": round(wl.packed.n_sets / (ms * 1e-3), 1),
                      "invalid_or_rejected_jobs": int((wl.expected != 1).sum())}
         b.free()
+        if not a.no_cpu_baseline:
+            # the CPU stand-in pool on the same workload (bounded sample, a few seconds); c4 is
+            # gossip (batchable), the block-shaped configs are one non-batchable call per block
+            try:
+                from oracle.cpu_pool import time_cpu_pool
+                c = time_cpu_pool(wl.packed, seconds=2.5, threads=a.cpu_threads, batchable=(name == "c4"))
+                per[name]["cpu_sets_per_s"] = c["value"]
+                per[name]["cpu_threads"] = c["cores"]
+            except Exception as e:  # reported, never fatal
+                per[name]["cpu_error"] = repr(e)
     out["per_config"] = per
     return out, wc1
 
