@@ -35,6 +35,12 @@
  *   aggregatePubkeys(engine, setPkOffsets: Uint32Array, pubkeys: Uint8Array)
  *     -> {out: Uint8Array, status: Int32Array}
  *   errorName(code: number) -> string
+ *   kzgLoadSetup(engine, g1: Uint8Array (48 B each), g2: Uint8Array (96 B each))   (throws on a bad point)
+ *   g1Lincomb(engine, scalars32le: Uint8Array, points48?: Uint8Array) -> Uint8Array(48)
+ *       (points omitted: the loaded setup's [tau^i] G1)
+ *   kzgVerifyProof(engine, commitment48, z32le, y32le, proof48) -> boolean
+ *   (the KZG calls are synchronous, as c-kzg's are; lodestar_amd/js/kzg.js builds the ckzg
+ *   module surface of util/kzg.ts on them)
  */
 #include <node_api.h>
 #include <stdint.h>
@@ -518,6 +524,78 @@ static napi_value g1_decompress(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+/* KZG group work (util/kzg.ts ckzg calls; synchronous, like c-kzg's) */
+static napi_value kzg_load_setup(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview g1, g2;
+  if (argc < 3 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &g1) || !g1.present || g1.type != napi_uint8_array || !g1.n || g1.n % 48 ||
+      !get_view(env, argv[2], &g2) || !g2.present || g2.type != napi_uint8_array || g2.n < 192 || g2.n % 96) {
+    napi_throw_type_error(env, NULL, "kzgLoadSetup(engine, g1: Uint8Array of 48-byte points, g2: Uint8Array of >= 2 96-byte points)");
+    return NULL;
+  }
+  const uint32_t n1 = (uint32_t)(g1.n / 48);
+  int32_t* st = (int32_t*)malloc((size_t)n1 * 4);
+  if (!st) return throw_code(env, LB_ERR_ARGUMENT);
+  const int32_t r = lb_kzg_load_setup(b->e, (const uint8_t*)g1.data, n1, (const uint8_t*)g2.data,
+                                      (uint32_t)(g2.n / 96), st);
+  free(st);
+  if (r != LB_OK) return throw_code(env, r);
+  napi_value u;
+  NAPI_CALL(env, napi_get_undefined(env, &u));
+  return u;
+}
+
+static napi_value g1_lincomb(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview sc, pts;
+  memset(&pts, 0, sizeof(pts));
+  if (argc < 2 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &sc) || !sc.present || sc.type != napi_uint8_array || sc.n % 32 ||
+      (argc >= 3 && !get_view(env, argv[2], &pts)) ||
+      (pts.present && (pts.type != napi_uint8_array || pts.n != sc.n / 32 * 48))) {
+    napi_throw_type_error(env, NULL, "g1Lincomb(engine, scalars32le: Uint8Array, points48?: Uint8Array)");
+    return NULL;
+  }
+  napi_value ab, out;
+  void* po;
+  NAPI_CALL(env, napi_create_arraybuffer(env, 48, &po, &ab));
+  const int32_t r = lb_g1_lincomb(b->e, (uint32_t)(sc.n / 32), pts.present ? (const uint8_t*)pts.data : NULL,
+                                  (const uint8_t*)sc.data, (uint8_t*)po);
+  if (r != LB_OK) return throw_code(env, r);
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, 48, ab, 0, &out));
+  return out;
+}
+
+static napi_value kzg_verify_proof(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview c, z, y, pr;
+  if (argc < 5 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &c) || !c.present || c.n != 48 || !get_view(env, argv[2], &z) || !z.present ||
+      z.n != 32 || !get_view(env, argv[3], &y) || !y.present || y.n != 32 || !get_view(env, argv[4], &pr) ||
+      !pr.present || pr.n != 48) {
+    napi_throw_type_error(env, NULL, "kzgVerifyProof(engine, commitment48, z32le, y32le, proof48)");
+    return NULL;
+  }
+  int32_t ok = 0;
+  const int32_t r = lb_kzg_verify_proof(b->e, (const uint8_t*)c.data, (const uint8_t*)z.data,
+                                        (const uint8_t*)y.data, (const uint8_t*)pr.data, &ok);
+  if (r != LB_OK) return throw_code(env, r);
+  if (ok < 0) return throw_code(env, -ok);
+  napi_value v;
+  NAPI_CALL(env, napi_get_boolean(env, ok == 1, &v));
+  return v;
+}
+
 static napi_value table_size(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], v;
@@ -550,6 +628,9 @@ static napi_value init(napi_env env, napi_value exports) {
       {"g1Decompress", NULL, g1_decompress, NULL, NULL, NULL, napi_default, NULL},
       {"aggregateSignatures", NULL, aggregate_signatures, NULL, NULL, NULL, napi_default, NULL},
       {"errorName", NULL, error_name, NULL, NULL, NULL, napi_default, NULL},
+      {"kzgLoadSetup", NULL, kzg_load_setup, NULL, NULL, NULL, napi_default, NULL},
+      {"g1Lincomb", NULL, g1_lincomb, NULL, NULL, NULL, napi_default, NULL},
+      {"kzgVerifyProof", NULL, kzg_verify_proof, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;
