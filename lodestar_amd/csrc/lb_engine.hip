@@ -124,6 +124,10 @@ struct lb_engine {
   uint32_t hash_g8_max = 2048;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
   uint32_t subgroup_g8_max = 4096;
+  // ... and S = sum r_i sig_i by per-set 8-lane scalar multiplications + trees instead of the
+  // bucket MSM (k_sig_blind_g8).  LB_SMALL_S_MAX.
+  uint32_t small_s_max = 32768;
+  dbuf s_terms, s_part;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -249,6 +253,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
+  if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -662,7 +667,25 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                            e->h_aff.as<uint32_t>());
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
-    {
+    if (n <= e->small_s_max) {
+      stage_scope sc(e, ST_SIG_MSM, s2);
+      LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
+      LB_HIP(e->s_part.ensure((size_t)((n + 63) / 64) * sizeof(g2j)));
+      hipLaunchKernelGGL(k_sig_blind_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                         e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                         e->s_terms.as<uint32_t>());
+      // 64:1 levels, ping-ponging between the two buffers; the last level writes treeS[1]
+      uint32_t* bufs[2] = {e->s_terms.as<uint32_t>(), e->s_part.as<uint32_t>()};
+      uint32_t m = n;
+      int cur = 0;
+      while (m > 64) {
+        const uint32_t mo = (m + 63) / 64;
+        hipLaunchKernelGGL(k_g2_sum64, dim3(mo), dim3(64), 0, s2, m, bufs[cur], mo, bufs[cur ^ 1], 0u);
+        m = mo;
+        cur ^= 1;
+      }
+      hipLaunchKernelGGL(k_g2_sum64, dim3(1), dim3(64), 0, s2, m, bufs[cur], 2 * mj, e->treeS.as<uint32_t>(), 1u);
+    } else {
       stage_scope sc(e, ST_SIG_MSM, s2);
       LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)LB_MSM_NB * 4, s2));
       LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)LB_MSM_NB * 4, s2));

@@ -765,6 +765,42 @@ __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restric
   }
 }
 
+// Small batches: S = sum r_i sig_i without the bucket MSM, whose chunk / bucket / reduction
+// chain is a fixed ~5 ms of serial G2 additions however few the sets.  Each live set's r_i sig_i
+// by 8 lanes (k_sig_blind_g8: GLV double-and-add, [lambda] sig = -psi^2(sig)), then 64:1 shuffle
+// trees (k_g2_sum64) into treeS element 1, where k_msm_reduce would have put it.
+__global__ void __launch_bounds__(64) k_sig_blind_g8(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                     const uint64_t* __restrict__ scalars,
+                                                     const uint32_t* __restrict__ set_live,
+                                                     const uint32_t* __restrict__ sig_inf,
+                                                     uint32_t* __restrict__ terms) {
+  const uint32_t i = blockIdx.x * 8 + (threadIdx.x >> 3);
+  if (i >= n) return;  // uniform within the group
+  g2j r = jac_infinity<fp2>();
+  if (msm_live(i, set_live, sig_inf)) {
+    const g2a a = soa_ld<g2a>(sig_aff, n, i);
+    const g2j t1 = jac_from_aff(a);
+    g2j t2 = g8_psi2(t1);
+    t2.y = fp2_neg(t2.y);  // [lambda] sig = -psi^2(sig)
+    g2j t3 = t1;
+    g8_add(t3, t2);
+    r = g8_mul_glv(t1, t2, t3, scalars[i]);
+  }
+  if (g8_q() == 0) soa_st(terms, n, i, r);
+}
+// element out0 + b of `out` (stride n_out) = sum of in[64 b .. 64 b + 63] (stride n_in)
+__global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* __restrict__ in, uint32_t n_out,
+                                                 uint32_t* __restrict__ out, uint32_t out0) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  g2j v = i < n_in ? soa_ld<g2j>(in, n_in, i) : jac_infinity<fp2>();
+  for (int l = 5; l >= 0; l--) {
+    const unsigned d = 1u << l;
+    const g2j o = g2j_shfl_down(v, d);
+    if (threadIdx.x < d) v = jac_add_i(v, o);
+  }
+  if (threadIdx.x == 0) soa_st(out, n_out, out0 + blockIdx.x, v);
+}
+
 // ---------------------------------------------------------------- invalid-set search
 // After a failing root check the engine searches for the failing sets over NODES: a node is a
 // contiguous range [lo_j, lo_j + len_j) of the members array (sets sorted by signing root) and
