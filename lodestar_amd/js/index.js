@@ -220,19 +220,25 @@ class BlsGpuVerifier {
    * @param {{batchable?: boolean, verifyOnMainThread?: boolean}} [opts]
    * @returns {Promise<boolean>}
    */
-  async verifySignatureSets(sets, opts) {
+  verifySignatureSets(sets, opts) {
+    // not `async`: a gossip call (one job of <= 128 sets) returns its job's own promise, so a call
+    // costs one promise instead of four (the per-call promise machinery dominated the JS side)
     opts = opts || {};
-    if (this.closed) throw new QueueError("QUEUE_ABORTED");
-    validateSets(sets);
-    if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
-      const res = addon.verifyJobsSync(this.engines[0], ...packJobs([sets]));
-      return codeToResult(res[0]);
+    try {
+      if (this.closed) throw new QueueError("QUEUE_ABORTED");
+      validateSets(sets);
+      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
+        const res = addon.verifyJobsSync(this.engines[0], ...packJobs([sets]));
+        return Promise.resolve(codeToResult(res[0]));
+      }
+    } catch (e) {
+      return Promise.reject(e);
     }
-    const results = await Promise.all(
+    // (an empty call is one empty job, which rejects with "Empty signature set" as in the reference)
+    if (sets.length < 2 * MAX_SIGNATURE_SETS_PER_JOB) return this.queueJob(sets, opts);
+    return Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) => this.queueJob(chunk, opts))
-    );
-    if (results.length === 0) throw Error("Empty results array");
-    return results.every((v) => v === true);
+    ).then((results) => results.every((v) => v === true));
   }
 
   async close() {
