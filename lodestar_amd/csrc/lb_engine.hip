@@ -127,6 +127,9 @@ struct lb_engine {
   // ... and S = sum r_i sig_i by per-set 8-lane scalar multiplications + trees instead of the
   // bucket MSM (k_sig_blind_g8).  LB_SMALL_S_MAX.
   uint32_t small_s_max = 32768;
+  // search rounds whose weighted sums cover at most this many positions skip the bucket MSM
+  // (k_smsm_terms_g8 + segmented sums).  LB_SEARCH_SMALL_MAX.
+  uint32_t search_small_max = 32768;
   dbuf s_terms, s_part;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -254,6 +257,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
+  if (const char* sm = getenv("LB_SEARCH_SMALL_MAX")) e->search_small_max = (uint32_t)strtoul(sm, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -786,7 +790,7 @@ enum {
   SX_KIND, SX_KEY, SX_LO, SX_LEN, SX_MIDX, SX_VERDICT, SX_Y, SX_PK,  // direct checks
   SX_MPRE, SX_MLO, SX_MMODE, SX_MWA, SX_MWB, SX_S,                     // MSM instances
   SX_TMODE, SX_TF, SX_TV0, SX_TU, SX_TMIDX, SX_TYIDX, SX_TLO, SX_TLEN, SX_TPER, SX_TOUT, SX_TPK, SX_YUP,
-  SX_ML, SX_COUNT
+  SX_ML, SX_BLO, SX_BHI, SX_BO, SX_COUNT
 };
 static_assert(SX_COUNT <= 32, "lb_engine::sx");
 struct test_job {
@@ -916,7 +920,32 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   auto U = [&](int k) { return e->sx[k].as<uint32_t>(); };
   {
     stage_scope sc(e, ST_FALLBACK, s1);
-    if (cm) {
+    if (cm && T && T <= e->search_small_max) {
+      // small round: per-position 8-lane terms + per-instance segmented sums (no bucket MSM)
+      std::vector<uint32_t> blo, bhi, bo{0};
+      for (uint32_t j = 0; j < cm; j++) {
+        for (uint32_t p = mpre[j]; p < mpre[j + 1]; p += 64) {
+          blo.push_back(p);
+          bhi.push_back(std::min(p + 64, mpre[j + 1]));
+        }
+        bo.push_back((uint32_t)blo.size());
+      }
+      const uint32_t nbk = (uint32_t)blo.size();
+      LB_HIP(sx_up(e, SX_BLO, blo, s1));
+      LB_HIP(sx_up(e, SX_BHI, bhi, s1));
+      LB_HIP(sx_up(e, SX_BO, bo, s1));
+      LB_HIP(e->s_terms.ensure((size_t)T * sizeof(g2j)));
+      LB_HIP(e->s_part.ensure((size_t)(nbk ? nbk : 1) * sizeof(g2j)));
+      const smsm_args ma{U(SX_MPRE), U(SX_MLO), U(SX_MMODE), U(SX_MWA), U(SX_MWB)};
+      hipLaunchKernelGGL(k_smsm_terms_g8, dim3((T + 7) / 8), dim3(64), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
+                         e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
+                         e->sig_inf.as<uint32_t>(), e->sig_aff.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
+      if (nbk)
+        hipLaunchKernelGGL(k_seg_sum64, dim3(nbk), dim3(64), 0, s1, U(SX_BLO), U(SX_BHI), T, e->s_terms.as<uint32_t>(),
+                           nbk, e->s_part.as<uint32_t>());
+      hipLaunchKernelGGL(k_seg_final, dim3(cm), dim3(64), 0, s1, U(SX_BO), e->s_part.as<uint32_t>(), nbk ? nbk : 1u,
+                         U(SX_S), cm);
+    } else if (cm) {
       LB_HIP(e->bcnt.ensure((size_t)nb * 4));
       LB_HIP(e->bcursor.ensure((size_t)nb * 4));
       LB_HIP(e->boff.ensure((size_t)(nb + 1) * 4));

@@ -212,13 +212,18 @@ __device__ __forceinline__ g2j g8_clear_cofactor(const g2j& p) {
 // [r] P for a blinding word w = hi:lo standing for r = lo + hi lambda (as jac_mul_glv_i):
 // t1 = P, t2 = [lambda] P, t3 = t1 + t2; 32 doublings and up to 32 additions, each addition of
 // the term the two bits select (one conditional g8_add per step, the term picked before it).
-__device__ __forceinline__ g2j g8_mul_glv(const g2j& t1, const g2j& t2, const g2j& t3, uint64_t w) {
+// [k0] t1 + [k1] t2 by one joint double-and-add over `bits` bits (t3 = t1 + t2)
+__device__ __forceinline__ g2j g8_mul_2d(const g2j& t1, const g2j& t2, const g2j& t3, uint64_t k0, uint64_t k1,
+                                         int bits) {
   g2j acc = jac_infinity<fp2>();
 #pragma clang loop unroll(disable)
-  for (int i = 31; i >= 0; i--) {
+  for (int i = bits - 1; i >= 0; i--) {
     g8_dbl(acc);
-    const uint32_t d = (uint32_t)((w >> i) & 1u) | ((uint32_t)((w >> (32 + i)) & 1u) << 1);
+    const uint32_t d = (uint32_t)((k0 >> i) & 1u) | ((uint32_t)((k1 >> i) & 1u) << 1);
     if (d) g8_add(acc, d == 1u ? t1 : (d == 2u ? t2 : t3));
   }
   return acc;
+}
+__device__ __forceinline__ g2j g8_mul_glv(const g2j& t1, const g2j& t2, const g2j& t3, uint64_t w) {
+  return g8_mul_2d(t1, t2, t3, w & 0xffffffffu, w >> 32, 32);
 }

@@ -889,6 +889,62 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c,
     }
   }
 }
+// Small search rounds (few thousand positions): the instances' weighted sums without the bucket
+// MSM, whose chunk / bucket / reduction chain is a fixed ~5 ms per round.  Position t's term
+// [w r_i] sig_i = [w lo] sig + [w hi] [lambda] sig (39-bit halves) by 8 lanes, then per-instance
+// sums: blocks of <= 64 positions of one instance (k_seg_sum64), then each instance's block sums
+// (k_seg_final, one wave).
+__global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, smsm_args a,
+                                                      const uint32_t* __restrict__ members,
+                                                      const uint32_t* __restrict__ set_uid,
+                                                      const uint64_t* __restrict__ scalars,
+                                                      const uint32_t* __restrict__ set_live,
+                                                      const uint32_t* __restrict__ sig_inf,
+                                                      const uint32_t* __restrict__ sig_aff, uint32_t n,
+                                                      uint32_t* __restrict__ terms) {
+  const uint32_t t = blockIdx.x * 8 + (threadIdx.x >> 3);
+  if (t >= T) return;  // uniform within the group
+  uint32_t j, i, wt;
+  smsm_member(a, c, t, members, set_uid, j, i, wt);
+  g2j r = jac_infinity<fp2>();
+  if (msm_live(i, set_live, sig_inf)) {
+    const g2j t1 = jac_from_aff(soa_ld<g2a>(sig_aff, n, i));
+    g2j t2 = g8_psi2(t1);
+    t2.y = fp2_neg(t2.y);  // [lambda] sig = -psi^2(sig)
+    g2j t3 = t1;
+    g8_add(t3, t2);
+    const uint64_t wd = scalars[i];
+    r = g8_mul_2d(t1, t2, t3, (wd & 0xffffffffu) * wt, (wd >> 32) * wt, 40);
+  }
+  if (g8_q() == 0) soa_st(terms, T, t, r);
+}
+// block b sums positions [blo[b], bhi[b]) (<= 64, one instance) -> part[b] (stride nb)
+__global__ void __launch_bounds__(64) k_seg_sum64(const uint32_t* __restrict__ blo, const uint32_t* __restrict__ bhi,
+                                                  uint32_t T, const uint32_t* __restrict__ terms, uint32_t nb,
+                                                  uint32_t* __restrict__ part) {
+  const uint32_t b = blockIdx.x, p = blo[b] + threadIdx.x;
+  g2j v = p < bhi[b] ? soa_ld<g2j>(terms, T, p) : jac_infinity<fp2>();
+  for (int l = 5; l >= 0; l--) {
+    const unsigned d = 1u << l;
+    const g2j o = g2j_shfl_down(v, d);
+    if (threadIdx.x < d) v = jac_add_i(v, o);
+  }
+  if (threadIdx.x == 0) soa_st(part, nb, b, v);
+}
+// instance j = sum of part[bo[j] .. bo[j+1]) -> out element j (stride n_out)
+__global__ void __launch_bounds__(64) k_seg_final(const uint32_t* __restrict__ bo, const uint32_t* __restrict__ part,
+                                                  uint32_t nb, uint32_t* __restrict__ out, uint32_t n_out) {
+  const uint32_t j = blockIdx.x;
+  g2j v = jac_infinity<fp2>();
+  for (uint32_t k = bo[j] + threadIdx.x; k < bo[j + 1]; k += 64) v = jac_add_i(v, soa_ld<g2j>(part, nb, k));
+  for (int l = 5; l >= 0; l--) {
+    const unsigned d = 1u << l;
+    const g2j o = g2j_shfl_down(v, d);
+    if (threadIdx.x < d) v = jac_add_i(v, o);
+  }
+  if (threadIdx.x == 0) soa_st(out, n_out, j, v);
+}
+
 // direct kind-1 nodes: Jacobian sum of r_i PK_i over the part's live members -> pk_out (SoA,
 // stride c)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,

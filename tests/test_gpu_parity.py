@@ -569,7 +569,8 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     lane per root (k_hash_finish, k_miller_grouped) and many lanes per root (k_hash_finish_g8:
     8-lane G2 doublings / additions; k_miller_wave: the wave engine); likewise the signatures'
     subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count) and S = sum r_i sig_i
-    (bucket MSM / per-set 8-lane scalar multiplications + trees, by set count).  Engines created with the
+    (bucket MSM / per-set 8-lane scalar multiplications + trees, by set count), and the invalid-set
+    search's weighted range sums (bucket MSM / per-position 8-lane terms + segmented sums).  Engines created with the
     thresholds at 0 and at 2^31 run the same batch (same blinding scalars) through each form;
     verdicts must match the planted expectation, and the root partials (576-byte Fp12 products
     before the final exponentiation) must be byte-identical."""
@@ -581,6 +582,7 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
         monkeypatch.setenv("LB_SUBGROUP_G8_MAX", lim)
         monkeypatch.setenv("LB_SMALL_S_MAX", lim)
+        monkeypatch.setenv("LB_SEARCH_SMALL_MAX", lim)
         with Engine(0) as e:
             wl = W.make(e, name)
             b = e.upload(W.indexed_for(e, wl))
