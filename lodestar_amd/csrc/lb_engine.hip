@@ -127,6 +127,7 @@ struct lb_engine {
   // ... and S = sum r_i sig_i by per-set 8-lane scalar multiplications + trees instead of the
   // bucket MSM (k_sig_blind_g8).  LB_SMALL_S_MAX.
   uint32_t small_s_max = 32768;
+  uint32_t small_s_g8_max = 2048;  // ... with 8 lanes per set up to here, one lane above (LB_SMALL_S_G8_MAX)
   // search rounds whose weighted sums cover at most this many positions skip the bucket MSM
   // (k_smsm_terms_g8 + segmented sums).  LB_SEARCH_SMALL_MAX.
   uint32_t search_small_max = 32768;
@@ -257,6 +258,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
+  if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
   if (const char* sm = getenv("LB_SEARCH_SMALL_MAX")) e->search_small_max = (uint32_t)strtoul(sm, nullptr, 10);
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
@@ -675,9 +677,14 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       stage_scope sc(e, ST_SIG_MSM, s2);
       LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
       LB_HIP(e->s_part.ensure((size_t)((n + 63) / 64) * sizeof(g2j)));
-      hipLaunchKernelGGL(k_sig_blind_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
-                         e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
-                         e->s_terms.as<uint32_t>());
+      if (n <= e->small_s_g8_max)
+        hipLaunchKernelGGL(k_sig_blind_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                           e->s_terms.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_sig_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                           e->s_terms.as<uint32_t>());
       // 64:1 levels, ping-ponging between the two buffers; the last level writes treeS[1]
       uint32_t* bufs[2] = {e->s_terms.as<uint32_t>(), e->s_part.as<uint32_t>()};
       uint32_t m = n;

@@ -788,6 +788,39 @@ __global__ void __launch_bounds__(64) k_sig_blind_g8(uint32_t n, const uint32_t*
   }
   if (g8_q() == 0) soa_st(terms, n, i, r);
 }
+// The same terms one lane per set, for mid-size batches (a slot of gossip): 8-lane groups at
+// ~20 k sets fill every SIMD's register file for ~5 ms and stall the per-root kernels of the
+// other stream.  r sig = [lo] sig + [hi] [lambda] sig by jac_mul_glv_i over the affine table
+// (sig, [lambda] sig, sig + [lambda] sig), the third made affine with one batched inversion per
+// block (as k_pk_blind does for G1).
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_sig_blind(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                          const uint64_t* __restrict__ scalars,
+                                                          const uint32_t* __restrict__ set_live,
+                                                          const uint32_t* __restrict__ sig_inf,
+                                                          uint32_t* __restrict__ terms) {
+  const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
+  const bool act = i < n && msm_live(i, set_live, sig_inf);
+  g2a t1{fp2_one(), fp2_one()}, t2 = t1;
+  g2j s = jac_infinity<fp2>();
+  if (act) {
+    t1 = soa_ld<g2a>(sig_aff, n, i);
+    t2 = g2a{fp2_mul_fp(t1.x, fp_load(LB_PSI2_CX)), fp2_neg(fp2_mul_fp(t1.y, fp_load(LB_PSI2_CY)))};
+    s = jac_add_aff_i<fp2, true>(jac_from_aff(t1), t2);  // finite: lambda + 1 != 0 mod r
+  }
+  const fp nz = fp_add(fp_sqr(s.z.c0), fp_sqr(s.z.c1));
+  const bool ok = act && !fp_is_zero(nz);
+  const fp ni = fp_inv_block(ok ? nz : fp_one());
+  if (i >= n) return;
+  g2j r = jac_infinity<fp2>();
+  if (ok) {
+    const fp2 zi{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
+    const fp2 zi2 = fp2_sqr(zi);
+    const g2a t3{fp2_mul(s.x, zi2), fp2_mul(fp2_mul(s.y, zi2), zi)};
+    r = jac_mul_glv_i<fp2, true>(t1, t2, t3, scalars[i]);
+  }
+  soa_st(terms, n, i, r);
+}
+
 // element out0 + b of `out` (stride n_out) = sum of in[64 b .. 64 b + 63] (stride n_in)
 __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* __restrict__ in, uint32_t n_out,
                                                  uint32_t* __restrict__ out, uint32_t out0) {

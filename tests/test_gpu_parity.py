@@ -568,20 +568,23 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
     lane per root (k_hash_finish, k_miller_grouped) and many lanes per root (k_hash_finish_g8:
     8-lane G2 doublings / additions; k_miller_wave: the wave engine); likewise the signatures'
-    subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count) and S = sum r_i sig_i
-    (bucket MSM / per-set 8-lane scalar multiplications + trees, by set count), and the invalid-set
-    search's weighted range sums (bucket MSM / per-position 8-lane terms + segmented sums).  Engines created with the
-    thresholds at 0 and at 2^31 run the same batch (same blinding scalars) through each form;
-    verdicts must match the planted expectation, and the root partials (576-byte Fp12 products
-    before the final exponentiation) must be byte-identical."""
+    subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count), S = sum r_i sig_i (bucket
+    MSM / per-set terms, one lane or 8 lanes per set, + trees, by set count) and the invalid-set
+    search's weighted range sums (bucket MSM / per-position 8-lane terms + segmented sums).
+    Engines created with the thresholds at 0 and at 2^31 run the same batch (same blinding
+    scalars) through each form; verdicts must match the planted expectation, and the root partials
+    (576-byte Fp12 products before the final exponentiation) must be byte-identical."""
     from lodestar_amd.engine import Engine
     from lodestar_amd import workloads as W
     outs = []
-    for lim in ("0", str(1 << 31)):
+    big = str(1 << 31)
+    # (all one-lane / MSM forms), (many-lane forms, one-lane S terms), (many-lane forms, 8-lane S terms)
+    for lim, s_g8 in (("0", "0"), (big, "0"), (big, big)):
         monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
         monkeypatch.setenv("LB_SUBGROUP_G8_MAX", lim)
         monkeypatch.setenv("LB_SMALL_S_MAX", lim)
+        monkeypatch.setenv("LB_SMALL_S_G8_MAX", s_g8)
         monkeypatch.setenv("LB_SEARCH_SMALL_MAX", lim)
         with Engine(0) as e:
             wl = W.make(e, name)
@@ -594,4 +597,4 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
                 b.free()
         assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
         outs.append(part)
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
