@@ -37,13 +37,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Each engine drives two HIP streams; HIP's default of 4 hardware queues per process would make
+# Each engine drives three HIP streams; HIP's default of 4 hardware queues per process would make
 # the streams of the batches in flight share queues (false dependencies between independent
-# batches).  16 queues (HIP reads this at runtime init, before any GPU call below) gives every
-# stream its own.  Measured on MI355X: profiles/r1_inflight_sweep.txt.  The GPU boxes export
-# GPU_MAX_HW_QUEUES=4, so raise it rather than only defaulting it.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# batches).  24 queues (HIP reads this at runtime init, before any GPU call below) gives each of
+# the 7 engines' 21 streams its own.  Measured on MI355X: profiles/r1_inflight_sweep.txt.  The GPU
+# boxes export GPU_MAX_HW_QUEUES=4, so raise it rather than only defaulting it.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 import numpy as np  # noqa: E402
 

@@ -102,7 +102,8 @@ struct lb_engine {
   int device = 0;
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
-  hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr;
+  hipStream_t stream3 = nullptr;  // s3: pubkey aggregation + blinding, beside the signature decode
+  hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr, ev_pk = nullptr;
   std::mutex mu;
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
@@ -264,9 +265,11 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
+    if (e->stream3) hipStreamDestroy(e->stream3);
     delete e;
     std::lock_guard<std::mutex> lk(g_engine_mu);
     g_engine_count[device]--;
@@ -276,6 +279,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   hipEventCreateWithFlags(&e->ev_s, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_dec, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_pk, hipEventDisableTiming);
   for (int i = 0; i < kStages; i++) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
@@ -294,7 +298,8 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
-                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root};
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root, &e->kzg_g1,
+                  &e->kzg_g2, &e->s_terms, &e->s_part};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
   for (int i = 0; i < kStages; i++) {
@@ -305,10 +310,13 @@ void lb_engine_destroy(lb_engine* e) {
   hipEventDestroy(e->ev_s);
   hipEventDestroy(e->ev_fork);
   hipEventDestroy(e->ev_dec);
+  hipEventDestroy(e->ev_pk);
   hipStreamSynchronize(e->stream2);
+  hipStreamSynchronize(e->stream3);
   if (e->scratch) delete e->scratch;
   if (e->h_nu) hipHostFree(e->h_nu);
   hipStreamDestroy(e->stream2);
+  hipStreamDestroy(e->stream3);
   hipStreamDestroy(e->stream);
   {
     std::lock_guard<std::mutex> lk(g_engine_mu);
@@ -586,7 +594,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     e->used[k] = false;
     e->acc_ms[k] = 0.f;
   }
-  hipStream_t s1 = e->stream, s2 = e->stream2;
+  hipStream_t s1 = e->stream, s2 = e->stream2, s3_ = e->stream3;
   if (e->profiling) {
     hipEventRecord(e->ev0[ST_TOTAL], s1);
     e->used[ST_TOTAL] = true;
@@ -595,26 +603,31 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   // fork: s2 starts after s1's scalar upload
   LB_HIP(hipEventRecord(e->ev_fork, s1));
   LB_HIP(hipStreamWaitEvent(s2, e->ev_fork, 0));
+  LB_HIP(hipStreamWaitEvent(s3_, e->ev_fork, 0));
   const uint32_t* nu = e->n_u.as<uint32_t>();
   if (n) {
-    // ---- s2: signatures, pubkeys, r*PK
+    // ---- pubkeys, r*PK: on s3 beside the signature decode for batches up to small_s_max sets
+    // (shortens the signature side's chain); on s2 before the decode for large batches, where the
+    // two would contend with the per-root chain on s1 for the whole chip
+    const hipStream_t s3 = n <= e->small_s_max ? s3_ : s2;
     {
-      stage_scope sc(e, ST_PK_CHUNKS, s2);
+      stage_scope sc(e, ST_PK_CHUNKS, s3);
       if (nc && b->indexed)
-        hipLaunchKernelGGL(k_pk_chunks_idx, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
+        hipLaunchKernelGGL(k_pk_chunks_idx, dim3(nblk(nc)), dim3(LB_TPB), 0, s3, nc, b->d_chunk_lo.as<uint32_t>(),
                            b->d_pks.as<uint32_t>(), e->table.as<uint32_t>(), e->table_cap,
                            e->table_flag.as<uint32_t>(), e->table_n, e->chunk_acc.as<uint32_t>(),
                            e->chunk_status.as<int32_t>());
       else if (nc)
-        hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s2, nc, b->d_chunk_lo.as<uint32_t>(),
+        hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s3, nc, b->d_chunk_lo.as<uint32_t>(),
                            b->d_pks.as<uint8_t>(), e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>());
     }
     {
-      stage_scope sc(e, ST_PK_BLIND, s2);
-      hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s2, n, nc, b->d_set_chunk_off.as<uint32_t>(),
+      stage_scope sc(e, ST_PK_BLIND, s3);
+      hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s3, n, nc, b->d_set_chunk_off.as<uint32_t>(),
                          e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
                          e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
     }
+    LB_HIP(hipEventRecord(e->ev_pk, s3));
     // signatures: decoded while s1 groups and hashes the messages
     {
       stage_scope sc(e, ST_DECODE, s2);
@@ -627,6 +640,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       else
         hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      LB_HIP(hipStreamWaitEvent(s2, e->ev_pk, 0));  // job statuses need the pubkey statuses
       hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s2, nj, b->d_job_off.as<uint32_t>(),
                          e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
                          e->set_live.as<uint32_t>());
@@ -1165,6 +1179,7 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
 
 static void finish_profile(lb_engine* e) {
   if (!e->profiling) return;
+  hipStreamSynchronize(e->stream3);
   hipStreamSynchronize(e->stream2);
   hipStreamSynchronize(e->stream);
   for (int k = 0; k < kStages; k++) {
