@@ -132,6 +132,8 @@ struct lb_engine {
   // search rounds whose weighted sums cover at most this many positions skip the bucket MSM
   // (k_smsm_terms_g8 + segmented sums).  LB_SEARCH_SMALL_MAX.
   uint32_t search_small_max = 32768;
+  // one launch pair per search round (look-ahead tests not skipped for passing checks)
+  bool search_merge = true;
   dbuf s_terms, s_part;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
@@ -261,6 +263,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
   if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
   if (const char* sm = getenv("LB_SEARCH_SMALL_MAX")) e->search_small_max = (uint32_t)strtoul(sm, nullptr, 10);
+  if (const char* sm = getenv("LB_SEARCH_MERGE")) e->search_merge = std::atoi(sm) != 0;
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -824,12 +827,19 @@ struct test_job {
 
 // children of a failing node: direct checks fan out to depth max(d + 1, min(d + 7, L - 6)) so a
 // weighted test of each failing child can reach the leaves; weighted tests to depth d + 6 (<= 64
-// children); a root's members in <= 64 parts
+// children); a root's members in <= 64 parts for direct checks (one FE each), in <= kWtParts
+// parts for a weighted test (one FE whatever f: a root of up to 1024 sets names its failing set
+// in one round)
+static constexpr uint32_t kWtParts = LB_WT_MAX;
+static uint32_t parts_per(uint32_t len, bool direct) {
+  const uint32_t f = direct ? 64u : kWtParts;
+  return (len + f - 1) / f;
+}
 static void search_children(const search_ctx& x, const snode& a, bool direct, std::vector<snode>& out) {
   out.clear();
   if (a.kind == 2u || a.len <= 1) return;
   auto parts = [&](uint32_t u, uint32_t lo, uint32_t len) {
-    const uint32_t per = (len + 63) / 64;
+    const uint32_t per = parts_per(len, direct);
     for (uint32_t q = 0; q < len; q += per) {
       const uint32_t l = per < len - q ? per : len - q;
       if (l == 1 && direct) out.push_back({2u, x.members[lo + q], lo + q, 1u, 0u});
@@ -897,7 +907,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       tv0[t] = c0.key;
       tm[t] = msm(a.lo, a.len, 1u, ulo0, span);
     } else {  // parts of one root
-      const uint32_t per = (a.len + 63) / 64;
+      const uint32_t per = parts_per(a.len, false);
       tmode[t] = 2u;
       tu[t] = c0.key;
       tper[t] = per;
@@ -1010,7 +1020,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   }
   {
     stage_scope sc(e, ST_BISECT, s1);
-    const srch_items I{c, nt, n_fresh, U(SX_KIND), U(SX_KEY), U(SX_MIDX), U(SX_TMODE), U(SX_TF), U(SX_TV0),
+    const srch_items I{c, nt, n_fresh, e->search_merge ? 0u : 1u, U(SX_KIND), U(SX_KEY), U(SX_MIDX), U(SX_TMODE), U(SX_TF), U(SX_TV0),
                        U(SX_TU), U(SX_TMIDX), U(SX_TYIDX)};
     auto stage = [&](uint32_t it0, uint32_t cnt) {
       if (!cnt) return;
@@ -1021,8 +1031,12 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       hipLaunchKernelGGL(k_search_fe, dim3(cnt), dim3(64), 0, s1, I, it0, cnt, U(SX_ML), U(SX_Y),
                          e->sx[SX_VERDICT].as<int32_t>());
     };
-    stage(0, c + n_fresh);        // direct checks and fresh tests
-    stage(c + n_fresh, nt - n_fresh);  // look-ahead tests of the failing direct checks
+    if (e->search_merge) {
+      stage(0, c + nt);
+    } else {
+      stage(0, c + n_fresh);             // direct checks and fresh tests
+      stage(c + n_fresh, nt - n_fresh);  // look-ahead tests of the failing direct checks
+    }
     if (nt) hipLaunchKernelGGL(k_search_match, dim3(nt), dim3(64), 0, s1, I, U(SX_YUP), U(SX_Y), e->sx[SX_TOUT].as<int32_t>());
   }
   LB_HIP(hipGetLastError());
