@@ -719,7 +719,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t*
 // Lane 0 of wave 0 combines the windows Horner-style: S = sum_w 2^(8w) W_w -> element out0 + j of
 // `out` (SoA, stride n_out).  The dependent chain is ~19 additions + 2 doublings + the Horner
 // doublings, against 34 additions + 12 doublings + the Horner for 16 lanes of 16 digits.  W = 4
-// (32-bit scalars) for the batch MSM, 5 for the search's weighted scalars (up to 40 bits).
+// (32-bit scalars) for the batch MSM, 6 for the search's weighted scalars (up to 43 bits).
 __device__ __forceinline__ g2j g2j_shfl_down(const g2j& a, unsigned d) {
   return g2j{fp2{fp_shfl_down(a.x.c0, d), fp_shfl_down(a.x.c1, d)},
              fp2{fp_shfl_down(a.y.c0, d), fp_shfl_down(a.y.c1, d)},
@@ -848,10 +848,12 @@ __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* 
 // T = sum len_j positions finds its instance by binary search of pre[]) with the scalar of set i
 // multiplied by a small weight: mode 0 weight 1 (S of a node), mode 1 (a weighted test over
 // subtrees of 2^b roots from root a) weight ((set_uid_i - a) >> b) + 1, mode 2 (a weighted test
-// over parts of a members) weight (position offset / a) + 1.  Weights are <= 128, so both
-// 32-bit GLV halves of r_i w stay below 2^40: LB_SMSM_W = 5 windows of 8 bits, instance j owning
-// buckets [j LB_SMSM_NB, (j+1) LB_SMSM_NB).
-#define LB_SMSM_W 5
+// over parts of a members) weight (position offset / a) + 1.  Weights are <= LB_WT_MAX, so
+// both 32-bit GLV halves of r_i w stay below 2^(32 + LB_WT_BITS) <= 2^48: LB_SMSM_W = 6 windows
+// of 8 bits, instance j owning buckets [j LB_SMSM_NB, (j+1) LB_SMSM_NB).
+#define LB_WT_MAX 1024  // children of a weighted test over parts of one root (lb_engine.hip kWtParts)
+#define LB_WT_BITS 11
+#define LB_SMSM_W 6
 #define LB_SMSM_NB (LB_SMSM_W * LB_MSM_B)
 __device__ __forceinline__ uint32_t rmsm_node(const uint32_t* __restrict__ pre, uint32_t c, uint32_t t) {
   uint32_t lo = 0, hi = c;  // pre[lo] <= t < pre[hi]
@@ -947,7 +949,7 @@ __global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, sm
     g2j t3 = t1;
     g8_add(t3, t2);
     const uint64_t wd = scalars[i];
-    r = g8_mul_2d(t1, t2, t3, (wd & 0xffffffffu) * wt, (wd >> 32) * wt, 40);
+    r = g8_mul_2d(t1, t2, t3, (wd & 0xffffffffu) * wt, (wd >> 32) * wt, 32 + LB_WT_BITS);
   }
   if (g8_q() == 0) soa_st(terms, T, t, r);
 }
@@ -996,7 +998,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, c
   soa_st(pk_out, c, j, acc);
 }
 // weighted tests over parts of one root (mode 2): sum_k (k + 1) sum_{i in part k} r_i PK_i,
-// one workgroup per test, lane k < f owning part k (64 lanes, two parts per lane above 64)
+// one workgroup per test, lane s owning parts k = s + 64 q (f <= LB_WT_MAX, q < 16): with A_q the
+// part sums, sum_q (s + 1 + 64 q) A_q = (s + 1) sum_q A_q + 64 sum_q q A_q, the last by running
+// sums (sum_q q A_q = sum_{j >= 1} sum_{q >= j} A_q): two additions per part and one 7-bit ladder
+// per lane instead of a ladder per part.
 __global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __restrict__ mode,
                                                 const uint32_t* __restrict__ tlo, const uint32_t* __restrict__ tlen,
                                                 const uint32_t* __restrict__ per, const uint32_t* __restrict__ members,
@@ -1006,22 +1011,28 @@ __global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __r
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (t >= nt || mode[t] != 2u) return;
   const uint32_t lo = tlo[t], len = tlen[t], pp = per[t];
-  g1j tot = jac_infinity<fp>();
-  for (uint32_t k = lane; k * pp < len; k += 64) {
-    g1j acc = jac_infinity<fp>();
-    const uint32_t a = lo + k * pp, e = lo + (k * pp + pp < len ? k * pp + pp : len);
-    for (uint32_t q = a; q < e; q++) {
-      const uint32_t i = members[q];
-      if (set_live[i]) acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));
+  const uint32_t nparts = (len + pp - 1) / pp;
+  g1j run = jac_infinity<fp>(), s1 = jac_infinity<fp>();
+  if (lane < nparts) {
+    const uint32_t qmax = (nparts - 1 - lane) / 64;
+    for (int q = (int)qmax; q >= 0; q--) {
+      const uint32_t k = lane + 64u * (uint32_t)q;
+      const uint32_t a = lo + k * pp, e = lo + (k * pp + pp < len ? k * pp + pp : len);
+      for (uint32_t x = a; x < e; x++) {
+        const uint32_t i = members[x];
+        if (set_live[i]) run = jac_add_i<fp, true>(run, soa_ld<g1j>(rpk, n, i));
+      }
+      if (q >= 1) s1 = jac_add_i<fp, true>(s1, run);
     }
-    g1j m = jac_infinity<fp>();
-    const uint32_t wt = k + 1;
-    for (int b = 7; b >= 0; b--) {
-      m = jac_dbl_i(m);
-      if ((wt >> b) & 1u) m = jac_add_i<fp, true>(m, acc);
-    }
-    tot = jac_add_i<fp, true>(tot, m);
   }
+  g1j tot = jac_infinity<fp>();
+  const uint32_t wt = lane + 1;  // <= 64: 7 bits
+  for (int b = 6; b >= 0; b--) {
+    tot = jac_dbl_i(tot);
+    if ((wt >> b) & 1u) tot = jac_add_i<fp, true>(tot, run);
+  }
+  for (int b = 0; b < 6; b++) s1 = jac_dbl_i(s1);
+  tot = jac_add_i<fp, true>(tot, s1);
   sh[lane] = tot;
   __syncthreads();
   for (uint32_t d = 32; d >= 1; d >>= 1) {
@@ -1111,15 +1122,17 @@ __device__ bool w_eq(fp* S, int a, int b) {
 //   mode 1: the children are f consecutive nodes v0 + k of the root product tree: P side
 //           prod_k treeP[v0 + k]^{k+1} by running products (2f Fp12 multiplications);
 //   mode 2: the children are parts of root u: P side ML(sum_k (k+1) PKsum_k, H_u) (k_test_pk).
-// A look-ahead test (t >= n_fresh) belongs to direct check tyidx[t] of the same round and is
-// skipped when that check passed (its y is 1): launched after k_search_fe of the direct checks.
+// A look-ahead test (t >= n_fresh) belongs to direct check tyidx[t] of the same round.  With
+// skip_ahead it is launched after k_search_fe of the direct checks and skipped when that check
+// passed (its y is 1): least work.  Without, everything is one launch pair: one FE latency less
+// per round (LB_SEARCH_MERGE), k_search_match ignoring the tests of passing checks.
 struct srch_items {
-  uint32_t c, nt, n_fresh;
+  uint32_t c, nt, n_fresh, skip_ahead;
   const uint32_t *kind, *key, *dmidx;                     // direct checks
   const uint32_t *tmode, *tf, *tv0, *tu, *tmidx, *tyidx;  // weighted tests
 };
 __device__ bool srch_skip(fp* S, const srch_items& I, uint32_t it, const uint32_t* __restrict__ ybuf) {
-  if (it < I.c + I.n_fresh) return false;
+  if (!I.skip_ahead || it < I.c + I.n_fresh) return false;
   w_load_soa12(S, LBW_A(6), ybuf, I.c + I.nt, I.tyidx[it - I.c]);
   return w_is_one(S, LBW_A(6));
 }
@@ -1209,12 +1222,20 @@ __global__ void __launch_bounds__(64) k_search_fe(srch_items I, uint32_t it0, ui
   w_store_soa12(S, LBW_A(0), ybuf, N, it);
   if (threadIdx.x == 0 && it < I.c) verdict[it] = one ? 1 : 0;
 }
+// z = y^k, 1 <= k <= f <= LB_WT_MAX, by baby steps / giant steps: baby[i] = y^(i+1) for i < m
+// (m = min(f, 32), in LDS), then w = z y^(-m j) for j = 0, 1, ... (y^-1 = conj(y): FE values lie
+// in the cyclotomic subgroup) compared by lanes i < m against baby[i] at once; k = m j + i + 1.
+// At most 32 + 32 Fp12 multiplications, against f for the plain walk.
+#define LB_BSGS_M 32
 __global__ void __launch_bounds__(64) k_search_match(srch_items I, const uint32_t* __restrict__ y_up,
                                                      const uint32_t* __restrict__ ybuf, int32_t* __restrict__ out_k) {
   LBW_SHARED(S);
+  __shared__ uint32_t baby[LB_BSGS_M][144];
+  __shared__ uint32_t s_hit;
   const uint32_t t = blockIdx.x;
   if (t >= I.nt) return;
   const uint32_t N = I.c + I.nt, f = I.tf[t];
+  const int lane = w_lane();
   w_init_consts(S);
   if (t < I.n_fresh) w_load_soa12(S, LBW_A(7), y_up, I.n_fresh, t);
   else w_load_soa12(S, LBW_A(7), ybuf, N, I.tyidx[t]);
@@ -1223,12 +1244,36 @@ __global__ void __launch_bounds__(64) k_search_match(srch_items I, const uint32_
     return;
   }
   w_load_soa12(S, LBW_A(0), ybuf, N, I.c + t);
-  if (t < I.n_fresh) w_load_soa12(S, LBW_A(1), y_up, I.n_fresh, t);
-  else w_load_soa12(S, LBW_A(1), ybuf, N, I.tyidx[t]);
+  const uint32_t m = f < LB_BSGS_M ? f : LB_BSGS_M;
+  w_conj(S, LBW_A(1), LBW_A(7));  // A1 runs over y^i (conj twice: a copy)
+  w_conj(S, LBW_A(1), LBW_A(1));
+  for (uint32_t i = 0; i < m; i++) {
+    if (lane < 12) {
+      const fp v = w_ld(S, LBW_A(1) + lane);
+      LB_UNROLL for (int w = 0; w < 12; w++) baby[i][12 * lane + w] = v.v[w];
+    }
+    w_sync();
+    if (i + 1 < m) w_mul(S, LBW_A(1), LBW_A(1), LBW_A(7));
+  }
+  w_conj(S, LBW_A(2), LBW_A(1));  // A1 = y^m after the loop: A2 = y^-m
   int hit = 0;
-  for (uint32_t k = 1; k <= f && !hit; k++) {
-    if (w_eq(S, LBW_A(0), LBW_A(1))) hit = (int)k;
-    else if (k < f) w_mul(S, LBW_A(1), LBW_A(1), LBW_A(7));
+  for (uint32_t j = 0; m * j < f && !hit; j++) {
+    if (lane == 0) s_hit = 0xffffffffu;
+    w_sync();
+    if ((uint32_t)lane < m) {
+      uint32_t d = 0;
+      for (int k = 0; k < 12; k++) {
+        const fp v = w_ld(S, LBW_A(0) + k);
+        LB_UNROLL for (int w = 0; w < 12; w++) d |= v.v[w] ^ baby[lane][12 * k + w];
+      }
+      const uint32_t kk = m * j + (uint32_t)lane + 1u;
+      if (d == 0 && kk <= f) atomicMin(&s_hit, kk);
+    }
+    w_sync();
+    const uint32_t h = s_hit;
+    w_sync();
+    if (h != 0xffffffffu) hit = (int)h;
+    else if (m * (j + 1) < f) w_mul(S, LBW_A(0), LBW_A(0), LBW_A(2));
   }
   if (threadIdx.x == 0) out_k[t] = hit;
 }

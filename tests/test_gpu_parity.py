@@ -497,10 +497,21 @@ def test_indexed_null_indices_only_without_keys(engine):
 
 
 def test_search_large_roots_parts_then_sets(engine):
-    """Roots with > 512 members are searched in 64 parts first (one Miller loop per part of the
-    blinded sum), then set by set; every planted wrong-message set is found."""
+    """Two roots of 750 members: one wrong set in root 0 is named by one weighted test over its
+    750 single-set parts (weights up to 750, baby-step / giant-step match); root 1's two wrong sets
+    fail that test and are searched in 64 direct parts, then set by set."""
     bad = {5, 777, 1400}
     jobs = make_shared_batch(engine, 1500, 2, seed=31, invalid=bad)
+    codes, prof = _verify_profiled(engine, jobs)
+    assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
+    assert prof["search_check"] > 0.0
+
+
+def test_search_root_above_weighted_part_cap(engine):
+    """Two roots of ~1100 members (> LB_WT_MAX = 1024 parts per weighted test): a weighted test runs
+    over parts of two sets, then over the named part's sets."""
+    bad = {3, 1099, 2150}
+    jobs = make_shared_batch(engine, 2200, 2, seed=37, invalid=bad)
     codes, prof = _verify_profiled(engine, jobs)
     assert [i for i, c in enumerate(codes) if c != 1] == sorted(bad)
     assert prof["search_check"] > 0.0
