@@ -135,6 +135,9 @@ struct lb_engine {
   // one launch pair per search round (look-ahead tests not skipped for passing checks)
   bool search_merge = true;
   dbuf s_terms, s_part;
+  // per-root signature sums for the search's root-level instances (LB_SEARCH_ROOTSUM)
+  dbuf s_root, rs_idx;
+  bool search_rootsum = true;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -264,6 +267,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
   if (const char* sm = getenv("LB_SEARCH_SMALL_MAX")) e->search_small_max = (uint32_t)strtoul(sm, nullptr, 10);
   if (const char* sm = getenv("LB_SEARCH_MERGE")) e->search_merge = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -302,7 +306,7 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
                   &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root, &e->kzg_g1,
-                  &e->kzg_g2, &e->s_terms, &e->s_part};
+                  &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
   for (int i = 0; i < kStages; i++) {
@@ -809,6 +813,7 @@ struct fnode {
 struct search_ctx {
   uint32_t n, nu, mu, L;
   std::vector<uint32_t> goff, members;
+  bool rs = false;  // e->s_root holds the per-root sums S_u
 };
 enum {
   SX_KIND, SX_KEY, SX_LO, SX_LEN, SX_MIDX, SX_VERDICT, SX_Y, SX_PK,  // direct checks
@@ -876,12 +881,23 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   const uint32_t c = (uint32_t)D.size(), nt = (uint32_t)tests.size(), n = x.n;
   std::vector<uint32_t> dk(c), dkey(c), dlo(c), dlen(c), dm(c, 0);
   std::vector<uint32_t> mlo, mpre{0}, mmode, mwa, mwb;
-  auto msm = [&](uint32_t lo, uint32_t len, uint32_t mode, uint32_t wa, uint32_t wb) {
+  // the same instances over whole roots (root-level form), while every instance is one
+  std::vector<uint32_t> rlo, rpre{0};
+  bool root_level = x.rs;
+  auto msm = [&](uint32_t lo, uint32_t len, uint32_t mode, uint32_t wa, uint32_t wb, const snode* whole) {
     mlo.push_back(lo);
     mpre.push_back(mpre.back() + len);
     mmode.push_back(mode);
     mwa.push_back(wa);
     mwb.push_back(wb);
+    if (whole && whole->kind == 0u) {
+      const uint32_t span = x.L - whole->d, ulo = (whole->key - (1u << whole->d)) << span;
+      const uint32_t uhi = std::min(x.nu, ulo + (1u << span));
+      rlo.push_back(ulo);
+      rpre.push_back(rpre.back() + (uhi - ulo));
+    } else {
+      root_level = false;
+    }
     return (uint32_t)mlo.size() - 1;
   };
   for (uint32_t j = 0; j < c; j++) {
@@ -889,7 +905,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
     dkey[j] = D[j].key;
     dlo[j] = D[j].lo;
     dlen[j] = D[j].len;
-    if (D[j].kind != 2u) dm[j] = msm(D[j].lo, D[j].len, 0u, 1u, 0u);
+    if (D[j].kind != 2u) dm[j] = msm(D[j].lo, D[j].len, 0u, 1u, 0u, &D[j]);
   }
   std::vector<uint32_t> tmode(nt), tf(nt), tv0(nt), tu(nt), tm(nt), tyi(nt), tlo(nt), tlen(nt), tper(nt);
   std::vector<uint32_t> yup((size_t)144 * (n_fresh ? n_fresh : 1));
@@ -905,18 +921,25 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       const uint32_t span = x.L - c0.d, ulo0 = (c0.key - (1u << c0.d)) << span;
       tmode[t] = 1u;
       tv0[t] = c0.key;
-      tm[t] = msm(a.lo, a.len, 1u, ulo0, span);
+      tm[t] = msm(a.lo, a.len, 1u, ulo0, span, &a);
     } else {  // parts of one root
       const uint32_t per = parts_per(a.len, false);
       tmode[t] = 2u;
       tu[t] = c0.key;
       tper[t] = per;
-      tm[t] = msm(a.lo, a.len, 2u, per, 0u);
+      tm[t] = msm(a.lo, a.len, 2u, per, 0u, nullptr);
     }
     if (T.fresh) {
       tyi[t] = t;  // fresh tests come first: y_up element t
       for (int q = 0; q < 144; q++) yup[(size_t)q * n_fresh + t] = F[T.src].y[q];
     }
+  }
+  // root-level round: every instance covers whole roots and the per-set form would take the
+  // bucket MSM; the instances then run over the per-root sums S_u (k_rsm_terms)
+  const bool rs_path = root_level && !mlo.empty() && mpre.back() > e->search_small_max;
+  if (rs_path) {
+    mlo.swap(rlo);
+    mpre.swap(rpre);
   }
   const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * LB_SMSM_NB;
   const uint32_t bcap = (2 * LB_SMSM_W * T) / LB_GROUP_CHUNK + nb;
@@ -951,8 +974,8 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   auto U = [&](int k) { return e->sx[k].as<uint32_t>(); };
   {
     stage_scope sc(e, ST_FALLBACK, s1);
-    if (cm && T && T <= e->search_small_max) {
-      // small round: per-position 8-lane terms + per-instance segmented sums (no bucket MSM)
+    if (cm && T && (rs_path || T <= e->search_small_max)) {
+      // small or root-level round: per-position terms + per-instance segmented sums (no bucket MSM)
       std::vector<uint32_t> blo, bhi, bo{0};
       for (uint32_t j = 0; j < cm; j++) {
         for (uint32_t p = mpre[j]; p < mpre[j + 1]; p += 64) {
@@ -968,12 +991,16 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       LB_HIP(e->s_terms.ensure((size_t)T * sizeof(g2j)));
       LB_HIP(e->s_part.ensure((size_t)(nbk ? nbk : 1) * sizeof(g2j)));
       const smsm_args ma{U(SX_MPRE), U(SX_MLO), U(SX_MMODE), U(SX_MWA), U(SX_MWB)};
-      hipLaunchKernelGGL(k_smsm_terms_g8, dim3((T + 7) / 8), dim3(64), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
-                         e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
-                         e->sig_inf.as<uint32_t>(), e->sig_aff.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
+      if (rs_path)
+        hipLaunchKernelGGL(k_rsm_terms, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->s_root.as<uint32_t>(), x.nu,
+                           e->s_terms.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_smsm_terms_g8, dim3((T + 7) / 8), dim3(64), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
+                           e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->sig_aff.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
       if (nbk)
         hipLaunchKernelGGL(k_seg_sum64, dim3(nbk), dim3(64), 0, s1, U(SX_BLO), U(SX_BHI), T, e->s_terms.as<uint32_t>(),
-                           nbk, e->s_part.as<uint32_t>());
+                           nbk, e->s_part.as<uint32_t>(), nullptr);
       hipLaunchKernelGGL(k_seg_final, dim3(cm), dim3(64), 0, s1, U(SX_BO), e->s_part.as<uint32_t>(), nbk ? nbk : 1u,
                          U(SX_S), cm);
     } else if (cm) {
@@ -1058,6 +1085,54 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   return LB_OK;
 }
 
+// S_u = sum r_i sig_i over the live sets of each root u (members order): the per-set terms one
+// lane per set (k_sig_blind), then segmented sums over each root's positions (blocks of <= 64 of
+// one root, then one wave per root).  Once per search, for large batches: the root-level
+// instances of a round (subtrees and weighted subtree tests) then cost a 7-bit multiple per ROOT.
+static int32_t search_root_sums(lb_engine* e, const search_ctx& x) {
+  hipStream_t s1 = e->stream;
+  const uint32_t n = x.n, nu = x.nu;
+  std::vector<uint32_t> idx;  // blo[nbk] | bhi[nbk] | bo[nu + 1]
+  std::vector<uint32_t> blo, bhi, bo{0};
+  for (uint32_t u = 0; u < nu; u++) {
+    for (uint32_t p = x.goff[u]; p < x.goff[u + 1]; p += 64) {
+      blo.push_back(p);
+      bhi.push_back(std::min(p + 64, x.goff[u + 1]));
+    }
+    bo.push_back((uint32_t)blo.size());
+  }
+  const uint32_t nbk = (uint32_t)blo.size();
+  idx.insert(idx.end(), blo.begin(), blo.end());
+  idx.insert(idx.end(), bhi.begin(), bhi.end());
+  idx.insert(idx.end(), bo.begin(), bo.end());
+  LB_HIP(e->rs_idx.ensure(idx.size() * 4));
+  LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
+  LB_HIP(e->s_part.ensure((size_t)(nbk ? nbk : 1) * sizeof(g2j)));
+  LB_HIP(e->s_root.ensure((size_t)nu * sizeof(g2j)));
+  LB_HIP(hipMemcpyAsync(e->rs_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s1));
+  const uint32_t* d_idx = e->rs_idx.as<uint32_t>();
+  {
+    stage_scope sc(e, ST_FALLBACK, s1);
+    hipLaunchKernelGGL(k_sig_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, e->sig_aff.as<uint32_t>(),
+                       e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                       e->s_terms.as<uint32_t>());
+    if (nbk)
+      hipLaunchKernelGGL(k_seg_sum64, dim3(nbk), dim3(64), 0, s1, d_idx, d_idx + nbk, n, e->s_terms.as<uint32_t>(), nbk,
+                         e->s_part.as<uint32_t>(), e->members.as<uint32_t>());
+    hipLaunchKernelGGL(k_seg_final, dim3(nu), dim3(64), 0, s1, d_idx + 2 * nbk, e->s_part.as<uint32_t>(),
+                       nbk ? nbk : 1u, e->s_root.as<uint32_t>(), nu);
+  }
+  LB_HIP(hipGetLastError());
+  LB_HIP(hipStreamSynchronize(s1));
+  if (e->profiling) {
+    float ms = 0.f;
+    if (e->used[ST_FALLBACK] && hipEventElapsedTime(&ms, e->ev0[ST_FALLBACK], e->ev1[ST_FALLBACK]) == hipSuccess)
+      e->acc_ms[ST_FALLBACK] += ms;
+    e->used[ST_FALLBACK] = false;
+  }
+  return LB_OK;
+}
+
 static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* out_job) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
   search_ctx x;
@@ -1073,6 +1148,11 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
   LB_HIP(hipMemcpyAsync(x.members.data(), e->members.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipMemcpyAsync(root.y.data(), e->y_root.p, 576, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipStreamSynchronize(e->stream));
+  if (e->search_rootsum && x.nu > 1 && n > e->search_small_max) {
+    const int32_t st = search_root_sums(e, x);
+    if (st != LB_OK) return st;
+    x.rs = true;
+  }
   std::vector<fnode> F{root};
   std::vector<uint32_t> bad_pos;
   auto condemn = [&](const snode& a) {

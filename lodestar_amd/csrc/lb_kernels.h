@@ -953,12 +953,13 @@ __global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, sm
   }
   if (g8_q() == 0) soa_st(terms, T, t, r);
 }
-// block b sums positions [blo[b], bhi[b]) (<= 64, one instance) -> part[b] (stride nb)
+// block b sums positions [blo[b], bhi[b]) (<= 64, one instance) -> part[b] (stride nb); the
+// term of position p is terms[perm ? perm[p] : p] (stride T)
 __global__ void __launch_bounds__(64) k_seg_sum64(const uint32_t* __restrict__ blo, const uint32_t* __restrict__ bhi,
                                                   uint32_t T, const uint32_t* __restrict__ terms, uint32_t nb,
-                                                  uint32_t* __restrict__ part) {
+                                                  uint32_t* __restrict__ part, const uint32_t* __restrict__ perm) {
   const uint32_t b = blockIdx.x, p = blo[b] + threadIdx.x;
-  g2j v = p < bhi[b] ? soa_ld<g2j>(terms, T, p) : jac_infinity<fp2>();
+  g2j v = p < bhi[b] ? soa_ld<g2j>(terms, T, perm ? perm[p] : p) : jac_infinity<fp2>();
   for (int l = 5; l >= 0; l--) {
     const unsigned d = 1u << l;
     const g2j o = g2j_shfl_down(v, d);
@@ -978,6 +979,28 @@ __global__ void __launch_bounds__(64) k_seg_final(const uint32_t* __restrict__ b
     if (threadIdx.x < d) v = jac_add_i(v, o);
   }
   if (threadIdx.x == 0) soa_st(out, n_out, j, v);
+}
+
+// Root-level search MSM (instances over whole roots: subtrees of the root product tree, modes 0
+// and 1): position t of instance j is root u = rlo_j + (t - pre_j) with weight 1 (mode 0) or
+// ((u - wa_j) >> wb_j) + 1 <= 64 (mode 1), term [w] S_u from the per-root sums S_u = sum r_i sig_i
+// (search_root_sums), one lane per position: 7 doublings + <= 7 additions instead of a 39-bit
+// weighted scalar per SET through the bucket MSM.
+__global__ void __launch_bounds__(LB_TPB) k_rsm_terms(uint32_t T, uint32_t c, smsm_args a,
+                                                      const uint32_t* __restrict__ s_root, uint32_t nu,
+                                                      uint32_t* __restrict__ terms) {
+  const uint32_t t = lb_tid();
+  if (t >= T) return;
+  const uint32_t j = rmsm_node(a.pre, c, t);
+  const uint32_t u = a.rlo[j] + (t - a.pre[j]);
+  const uint32_t wt = a.mode[j] == 0u ? 1u : ((u - a.wa[j]) >> a.wb[j]) + 1u;
+  const g2j su = soa_ld<g2j>(s_root, nu, u);
+  g2j r = jac_infinity<fp2>();
+  for (int b = 6; b >= 0; b--) {
+    r = jac_dbl_i(r);
+    if ((wt >> b) & 1u) r = jac_add_i<fp2, true>(r, su);
+  }
+  soa_st(terms, T, t, r);
 }
 
 // direct kind-1 nodes: Jacobian sum of r_i PK_i over the part's live members -> pk_out (SoA,
