@@ -136,8 +136,9 @@ struct lb_engine {
   bool search_merge = true;
   dbuf s_terms, s_part;
   // per-root signature sums for the search's root-level instances (LB_SEARCH_ROOTSUM)
-  dbuf s_root, rs_idx;
+  dbuf s_root, rs_idx, s_set;
   bool search_rootsum = true;
+  bool search_pre = false;  // later rounds take [w] of the kept per-set terms (LB_SEARCH_PRE)
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -268,6 +269,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_SMALL_MAX")) e->search_small_max = (uint32_t)strtoul(sm, nullptr, 10);
   if (const char* sm = getenv("LB_SEARCH_MERGE")) e->search_merge = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -306,7 +308,7 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
                   &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root, &e->kzg_g1,
-                  &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx};
+                  &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
   for (int i = 0; i < kStages; i++) {
@@ -974,7 +976,8 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   auto U = [&](int k) { return e->sx[k].as<uint32_t>(); };
   {
     stage_scope sc(e, ST_FALLBACK, s1);
-    if (cm && T && (rs_path || T <= e->search_small_max)) {
+    const bool pre = x.rs && e->search_pre;
+    if (cm && T && (rs_path || pre || T <= e->search_small_max)) {
       // small or root-level round: per-position terms + per-instance segmented sums (no bucket MSM)
       std::vector<uint32_t> blo, bhi, bo{0};
       for (uint32_t j = 0; j < cm; j++) {
@@ -994,6 +997,9 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       if (rs_path)
         hipLaunchKernelGGL(k_rsm_terms, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->s_root.as<uint32_t>(), x.nu,
                            e->s_terms.as<uint32_t>());
+      else if (pre)  // the per-set terms r_i sig_i are kept from search_root_sums
+        hipLaunchKernelGGL(k_smsm_terms_pre, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
+                           e->set_uid.as<uint32_t>(), e->s_set.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
       else
         hipLaunchKernelGGL(k_smsm_terms_g8, dim3((T + 7) / 8), dim3(64), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
                            e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
@@ -1106,7 +1112,7 @@ static int32_t search_root_sums(lb_engine* e, const search_ctx& x) {
   idx.insert(idx.end(), bhi.begin(), bhi.end());
   idx.insert(idx.end(), bo.begin(), bo.end());
   LB_HIP(e->rs_idx.ensure(idx.size() * 4));
-  LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
+  LB_HIP(e->s_set.ensure((size_t)n * sizeof(g2j)));
   LB_HIP(e->s_part.ensure((size_t)(nbk ? nbk : 1) * sizeof(g2j)));
   LB_HIP(e->s_root.ensure((size_t)nu * sizeof(g2j)));
   LB_HIP(hipMemcpyAsync(e->rs_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s1));
@@ -1115,9 +1121,9 @@ static int32_t search_root_sums(lb_engine* e, const search_ctx& x) {
     stage_scope sc(e, ST_FALLBACK, s1);
     hipLaunchKernelGGL(k_sig_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s1, n, e->sig_aff.as<uint32_t>(),
                        e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
-                       e->s_terms.as<uint32_t>());
+                       e->s_set.as<uint32_t>());
     if (nbk)
-      hipLaunchKernelGGL(k_seg_sum64, dim3(nbk), dim3(64), 0, s1, d_idx, d_idx + nbk, n, e->s_terms.as<uint32_t>(), nbk,
+      hipLaunchKernelGGL(k_seg_sum64, dim3(nbk), dim3(64), 0, s1, d_idx, d_idx + nbk, n, e->s_set.as<uint32_t>(), nbk,
                          e->s_part.as<uint32_t>(), e->members.as<uint32_t>());
     hipLaunchKernelGGL(k_seg_final, dim3(nu), dim3(64), 0, s1, d_idx + 2 * nbk, e->s_part.as<uint32_t>(),
                        nbk ? nbk : 1u, e->s_root.as<uint32_t>(), nu);

@@ -1003,6 +1003,27 @@ __global__ void __launch_bounds__(LB_TPB) k_rsm_terms(uint32_t T, uint32_t c, sm
   soa_st(terms, T, t, r);
 }
 
+// The set-level instances of a round once the per-set terms T_i = r_i sig_i exist (search_root_sums
+// keeps them): position t's term is [w] T_i, w <= LB_WT_MAX, by an LB_WT_BITS-bit ladder in one lane
+// instead of the 43-bit weighted scalar by 8 lanes (k_smsm_terms_g8).
+__global__ void __launch_bounds__(LB_TPB) k_smsm_terms_pre(uint32_t T, uint32_t c, smsm_args a,
+                                                           const uint32_t* __restrict__ members,
+                                                           const uint32_t* __restrict__ set_uid,
+                                                           const uint32_t* __restrict__ set_terms, uint32_t n,
+                                                           uint32_t* __restrict__ terms) {
+  const uint32_t t = lb_tid();
+  if (t >= T) return;
+  uint32_t j, i, wt;
+  smsm_member(a, c, t, members, set_uid, j, i, wt);
+  const g2j ti = soa_ld<g2j>(set_terms, n, i);  // infinity for a set outside the equation
+  g2j r = jac_infinity<fp2>();
+  for (int b = LB_WT_BITS - 1; b >= 0; b--) {
+    r = jac_dbl_i(r);
+    if ((wt >> b) & 1u) r = jac_add_i<fp2, true>(r, ti);
+  }
+  soa_st(terms, T, t, r);
+}
+
 // direct kind-1 nodes: Jacobian sum of r_i PK_i over the part's live members -> pk_out (SoA,
 // stride c)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,
