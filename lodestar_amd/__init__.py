@@ -7,6 +7,7 @@ from .verifier import (  # noqa: F401
     BlsGpuVerifier,
     PublicKey,
     QueueError,
+    QueueErrorCode,
     SignatureSetType,
     SingleSignatureSet,
     VerifySignatureOpts,

@@ -12,8 +12,17 @@
 #pragma once
 #include "lb_kernels.h"
 
+// [r] P == O for an affine G1 point (r = the BLS12-381 subgroup order): the G1 subgroup check of
+// points that come from the wire (KZG commitments and proofs of gossip blob sidecars; c-kzg's
+// validate_kzg_g1 rejects the same points)
+__device__ __forceinline__ bool g1_in_subgroup_r(const g1a& a) {
+  const uint32_t rr[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                          0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  return jac_is_inf(jac_mul_u256(a, rr));
+}
+
 // one point per thread: P_i (table entry i, or 48 compressed bytes) times scalar i (32 bytes,
-// little endian, < r) -> Jacobian SoA terms
+// little endian, < r) -> Jacobian SoA terms.  Given points are curve- and subgroup-checked.
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_terms(uint32_t n, const uint8_t* __restrict__ pts48,
                                                      const uint32_t* __restrict__ table, uint32_t table_cap,
                                                      const uint32_t* __restrict__ scalars,
@@ -27,6 +36,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_terms(uint32_t n, const 
     uint8_t b[48];
     ld_bytes<48>(b, pts48 + (size_t)48 * i);
     st = g1_decompress48(b, p, inf);
+    if (st == LB_OK && !inf && !g1_in_subgroup_r(p)) st = LB_POINT_NOT_IN_GROUP;
   } else {
     p = soa_ld<g1a>(table, table_cap, i);
   }
@@ -103,14 +113,15 @@ __global__ void __launch_bounds__(64) k_kzg_setup_g2(const uint8_t* __restrict__
 
 // verify_kzg_proof_impl: e(C - [y] G1, -G2) e(pi, [tau] G2 - [z] G2) == 1, rewritten with the
 // scalar moved to G1 (bilinearity): e(Q, -G2) e(pi, [tau] G2) == 1 with Q = C - [y] G1 + [z] pi.
-// Lanes 0 and 1 compute [y] G1 and [z] pi side by side; the two Miller loops and the final
+// Lanes 0 and 1 compute [y] G1 and [z] pi side by side, lanes 2 and 3 the subgroup checks of C
+// and pi (c-kzg rejects commitments and proofs outside G1); the two Miller loops and the final
 // exponentiation run on the wave engine.  io[0..47] C, [48..95] pi, scalars y, z (8 LE words
 // each); g2 = [tau^0] G2, [tau^1] G2 (g2a).  *ok = 1 / 0, or -code for a bad point encoding.
 __global__ void __launch_bounds__(64) k_kzg_check(const uint8_t* __restrict__ io, const uint32_t* __restrict__ yz,
                                                   const uint32_t* __restrict__ g2, int32_t* __restrict__ ok) {
   LBW_SHARED_ML(S);
   __shared__ g1j sh[2];
-  __shared__ int st_sh, qinf_sh, pinf_sh;
+  __shared__ int st_sh, qinf_sh, pinf_sh, grp_sh[2];
   const int lane = threadIdx.x;
   w_init_consts(S, LBW_PROGS_ALL);
   g1a c, pi;
@@ -131,8 +142,13 @@ __global__ void __launch_bounds__(64) k_kzg_check(const uint8_t* __restrict__ io
     const g1a base = lane == 0 ? g1a{fp_load(LB_G1X), fp_load(LB_G1Y)} : pi;
     const bool binf = lane == 1 && pinf;
     sh[lane] = (st == LB_OK && !binf) ? jac_mul_u256(base, k) : jac_infinity<fp>();
+  } else if (lane < 4) {
+    const bool isc = lane == 2;
+    const bool skip = st != LB_OK || (isc ? cinf : pinf);
+    grp_sh[lane - 2] = skip || g1_in_subgroup_r(isc ? c : pi) ? 1 : 0;
   }
   __syncthreads();
+  if (st == LB_OK && !(grp_sh[0] && grp_sh[1])) st = LB_POINT_NOT_IN_GROUP;
   if (lane == 0) {
     g1j q = cinf ? jac_infinity<fp>() : jac_from_aff(c);
     q = jac_add_i(q, jac_neg(sh[0]));

@@ -2,7 +2,14 @@
 // Mirrors packages/beacon-node/src/chain/bls/interface.ts:3-46 and
 // packages/state-transition/src/util/signatureSets.ts:5-22.
 
-export type PublicKeyLike = Uint8Array | GpuPublicKey | {toBytes(): Uint8Array};
+/** @chainsafe/bls PointFormat */
+export declare const PointFormat: {compressed: "compressed"; uncompressed: "uncompressed"};
+
+/**
+ * A registered handle, a @chainsafe/bls PublicKey (serialised with toBytes("uncompressed"); a
+ * 48-byte result is decompressed on the GPU), or raw 96- / 48-byte encodings.
+ */
+export type PublicKeyLike = Uint8Array | GpuPublicKey | {toBytes(format?: "compressed" | "uncompressed"): Uint8Array};
 
 export declare const SignatureSetType: {single: "single"; aggregate: "aggregate"};
 
@@ -20,8 +27,17 @@ export interface IBlsVerifier {
   close(): Promise<void>;
 }
 
+/** beacon-node/src/util/queue/errors.ts:3-6 */
+export declare const QueueErrorCode: {
+  QUEUE_ABORTED: "QUEUE_ERROR_QUEUE_ABORTED";
+  QUEUE_MAX_LENGTH: "QUEUE_ERROR_QUEUE_MAX_LENGTH";
+};
+
+/** LodestarError<{code}>: message = type.code */
 export declare class QueueError extends Error {
+  constructor(type: {code: string});
   type: {code: string};
+  getMetadata(): {code: string};
 }
 
 /** A key registered in the GPU-resident table (the epoch cache's index2pubkey entry). */
@@ -32,7 +48,9 @@ export declare class GpuPublicKey {
 
 export declare class BlsGpuVerifier implements IBlsVerifier {
   /** engines: batches in flight on the device (default 2), each with its own streams + workspace */
-  constructor(opts?: {device?: number; engines?: number; blsVerifyAllMultiThread?: boolean});
+  /** modules as BlsMultiThreadWorkerPool's: metrics.blsThreadPool.* / metrics.bls.* get the same updates */
+  constructor(opts?: {device?: number; engines?: number; blsVerifyAllMultiThread?: boolean},
+              modules?: {logger?: {error(msg: string, ctx?: object, e?: Error): void}; metrics?: unknown});
   /** 48- or 96-byte keys -> handles carrying their table index (validate: keyValidate checks) */
   registerPubkeys(keys: Uint8Array[], validate?: boolean): GpuPublicKey[];
   verifySignatureSets(sets: ISignatureSet[], opts?: VerifySignatureOpts): Promise<boolean>;
@@ -41,7 +59,8 @@ export declare class BlsGpuVerifier implements IBlsVerifier {
   /** bls.Signature.aggregate(signatures).toBytes() (op pools), 96-byte compressed */
   aggregateSignatures(signatures: Uint8Array[], validate?: boolean): Uint8Array;
   close(): Promise<void>;
-  readonly stats: {batches: number; jobs: number; sets: number; jobsInvalid: number; jobsError: number};
+  readonly stats: {batches: number; jobs: number; sets: number; batchRetries: number; batchSigsSuccess: number;
+    jobsInvalid: number; jobsError: number; jobWaitMs: number; deviceMs: number; mainThreadMs: number};
 }
 
 /** light-client isValidBlsAggregate (validation.ts:154-184) with its stage-prefixed errors */

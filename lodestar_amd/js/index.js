@@ -20,11 +20,20 @@
  *   - a handle returned by registerPubkeys() (the epoch cache's index2pubkey entries,
  *     state-transition/src/cache/pubkeyCache.ts:56-77): it carries its index into the
  *     GPU-resident key table, and packages whose keys all have one ship 4-byte indices;
- *   - or anything with `toBytes()` returning the 96-byte uncompressed encoding (what the reference
- *     main thread sends to workers: getAggregatedPubkey(s).toBytes(PointFormat.uncompressed),
- *     multithread/index.ts:160), or a 96-byte Uint8Array.
- * Malformed inputs (root not 32 bytes, pubkey not 96 bytes, signature not a Uint8Array) reject
- * only the call that carries them, before anything is queued.
+ *   - or a `@chainsafe/bls` `PublicKey` (anything with `toBytes(format)`): it is serialised with
+ *     `toBytes("uncompressed")`, exactly as the reference main thread does before posting to a
+ *     worker (getAggregatedPubkey(s).toBytes(PointFormat.uncompressed), multithread/index.ts:126,160).
+ *     An object whose toBytes ignores the format and returns the 48-byte compressed default is
+ *     decompressed on the GPU.  The 96 bytes are cached per key object (WeakMap), so a long-lived
+ *     index2pubkey entry is serialised once, not once per call;
+ *   - or a 96-byte (uncompressed) or 48-byte (compressed) Uint8Array.
+ * Malformed inputs (root not 32 bytes, pubkey of another length, signature not a Uint8Array)
+ * reject only the call that carries them, before anything is queued.
+ *
+ * Synchronous entry points (verifyOnMainThread, verifySignatureSet, aggregateSignatures, key
+ * decompression) run on their own engine, outside the async pool, so a main-thread call never
+ * waits behind a gossip batch holding a pool engine (the reference runs them on the main thread
+ * while workers are busy, multithread/index.ts:138-151).
  */
 const path = require("path");
 
@@ -36,10 +45,19 @@ const MAX_BUFFER_WAIT_MS = 100;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
 
+/** beacon-node/src/util/queue/errors.ts:3-14 (a LodestarError: message = type.code, utils/src/errors.ts:6-8) */
+const QueueErrorCode = {
+  QUEUE_ABORTED: "QUEUE_ERROR_QUEUE_ABORTED",
+  QUEUE_MAX_LENGTH: "QUEUE_ERROR_QUEUE_MAX_LENGTH",
+};
+
 class QueueError extends Error {
-  constructor(code) {
-    super(code);
-    this.type = {code: code};
+  constructor(type) {
+    super(type.code);
+    this.type = type;
+  }
+  getMetadata() {
+    return this.type;
   }
 }
 
@@ -53,9 +71,29 @@ function chunkifyMaximizeChunkSize(arr, minPerChunk) {
   return out;
 }
 
+/** PointFormat of @chainsafe/bls (its toBytes default is compressed, 48 bytes) */
+const PointFormat = {compressed: "compressed", uncompressed: "uncompressed"};
+
+// 96-byte uncompressed encodings of PublicKey objects seen before (index2pubkey entries live for
+// the epoch cache's lifetime; the reference pays toBytes(uncompressed) on every call)
+const pkCache = new WeakMap();
+
+/** The 96- or 48-byte encoding of one key (48 only if its toBytes ignores the format argument). */
+function pkRawBytes(pk) {
+  if (pk instanceof Uint8Array) return pk;
+  if (pk === null || typeof pk !== "object" || typeof pk.toBytes !== "function") throw Error("pubkey must be a PublicKey or Uint8Array");
+  const hit = pkCache.get(pk);
+  if (hit) return hit;
+  const b = pk.toBytes(PointFormat.uncompressed);
+  if (!(b instanceof Uint8Array) || (b.length !== 96 && b.length !== 48)) throw Error("pubkey must be 48 or 96 bytes");
+  if (b.length === 96) pkCache.set(pk, b);
+  return b;
+}
+
+/** 96-byte encoding of a key already normalised by normalizeKeys (packJobs only) */
 function pkBytes(pk) {
-  const b = pk instanceof Uint8Array ? pk : pk.toBytes();
-  if (!(b instanceof Uint8Array) || b.length !== 96) throw Error("pubkey must be 96-byte uncompressed");
+  const b = pkRawBytes(pk);
+  if (b.length !== 96) throw Error("pubkey must be 96-byte uncompressed");
   return b;
 }
 
@@ -65,16 +103,42 @@ function setPubkeys(s) {
   throw Error("Unknown signature set type");
 }
 
-/** Checks one call's sets before queueing: a malformed set rejects only its own call. */
-function validateSets(sets) {
-  for (const s of sets) {
+/**
+ * Checks one call's sets before queueing (a malformed set rejects only its own call) and returns
+ * the sets with every 48-byte key replaced by its 96-byte form: compressed keys of the call are
+ * decompressed on the GPU in one batch by `decompress(flat48) -> {out, status}`; a key that does not
+ * decode rejects the call with its blst error.
+ */
+function normalizeSets(sets, decompress) {
+  let short = null;  // [setIndex, keyIndex | -1, bytes48]
+  sets.forEach((s, si) => {
     const pks = setPubkeys(s);
     if (!Array.isArray(pks)) throw Error("aggregate set needs a pubkeys array");
-    for (const pk of pks) if (!(pk instanceof GpuPublicKey)) pkBytes(pk);
+    pks.forEach((pk, ki) => {
+      if (pk instanceof GpuPublicKey) return;
+      const b = pkRawBytes(pk);
+      if (b.length === 48) (short = short || []).push([si, s.type === SignatureSetType.single ? -1 : ki, b, pk]);
+    });
     const root = s.signingRoot;
     if (!root || root.length !== 32) throw Error("signing root must be 32 bytes");
     if (!(s.signature instanceof Uint8Array)) throw Error("signature must be a Uint8Array");
-  }
+  });
+  if (short === null) return sets;
+  const flat = new Uint8Array(48 * short.length);
+  short.forEach(([, , b], k) => flat.set(b, 48 * k));
+  const d = decompress(flat);
+  d.status.forEach((st) => {
+    if (st !== 0) throw Error(addon.errorName(st));
+  });
+  const out = sets.slice();
+  short.forEach(([si, ki, , pk], k) => {
+    const b96 = d.out.subarray(96 * k, 96 * k + 96);
+    if (!(pk instanceof Uint8Array)) pkCache.set(pk, b96);
+    if (out[si] === sets[si]) out[si] = ki < 0 ? {...sets[si]} : {...sets[si], pubkeys: sets[si].pubkeys.slice()};
+    if (ki < 0) out[si].pubkey = b96;
+    else out[si].pubkeys[ki] = b96;
+  });
+  return out;
 }
 
 /** A public key registered in the GPU-resident table (index2pubkey entry). */
@@ -136,20 +200,41 @@ function codeToResult(code) {
 class BlsGpuVerifier {
   /**
    * @param {{device?: number, engines?: number, blsVerifyAllMultiThread?: boolean}} [opts]
+   * @param {{logger?: object, metrics?: object|null}} [modules] as the reference pool's
+   *   (multithread/index.ts:98-134): `metrics.blsThreadPool.*` / `metrics.bls.*` receive the same
+   *   updates (lodestar.ts:433-523) when given
    */
-  constructor(opts) {
+  constructor(opts, modules) {
     opts = opts || {};
+    modules = modules || {};
     const n = opts.engines === undefined ? 2 : opts.engines;
     if (!(n >= 1)) throw Error("engines must be >= 1");
+    const device = opts.device === undefined ? 0 : opts.device;
     this.engines = [];
-    for (let k = 0; k < n; k++) this.engines.push(addon.createEngine(opts.device === undefined ? 0 : opts.device));
+    try {
+      for (let k = 0; k < n; k++) this.engines.push(addon.createEngine(device));
+      // synchronous calls get their own engine: never queued behind a pool batch's engine mutex
+      this.syncEngine = addon.createEngine(device);
+    } catch (e) {
+      for (const en of this.engines) addon.destroyEngine(en);
+      throw e;
+    }
     this.idle = this.engines.slice();
     this.blsVerifyAllMultiThread = Boolean(opts.blsVerifyAllMultiThread);
+    this.logger = modules.logger || null;
+    this.metrics = modules.metrics || null;
     this.jobs = [];
     this.buffered = null;
     this.running = new Set();
     this.closed = false;
-    this.stats = {batches: 0, jobs: 0, sets: 0, batchRetries: 0, jobsInvalid: 0, jobsError: 0};
+    this.stats = {batches: 0, jobs: 0, sets: 0, batchRetries: 0, batchSigsSuccess: 0, jobsInvalid: 0, jobsError: 0,
+      jobWaitMs: 0, deviceMs: 0, mainThreadMs: 0};
+    this.decompress = (flat48) => addon.g1Decompress(this.syncEngine, flat48);
+  }
+
+  /** every engine, the synchronous one included (they share one key-table layout) */
+  allEngines() {
+    return this.syncEngine ? [this.syncEngine, ...this.engines] : this.engines;
   }
 
   /**
@@ -170,18 +255,28 @@ class BlsGpuVerifier {
     });
     if (size === 48) {
       // decompressed once on the GPU: handles keep the 96-byte form for byte-carrying packages
-      const d = addon.g1Decompress(this.engines[0], flat);
+      const d = this.decompress(flat);
       for (const st of d.status) if (st !== 0) throw Error(addon.errorName(st));
       flat = d.out;
     }
     let first = -1;
-    for (const e of this.engines) {
+    for (const e of this.allEngines()) {
       const r = addon.registerPubkeys(e, flat, 96, Boolean(validate));
       for (const st of r.status) if (st !== 0) throw Error(addon.errorName(st));
       if (first >= 0 && r.first !== first) throw Error("engine pubkey tables out of step");
       first = r.first;
     }
     return keys.map((k, i) => new GpuPublicKey(first + i, flat.subarray(96 * i, 96 * i + 96)));
+  }
+
+  /** one job verified synchronously on the caller's thread (the reference's main-thread path) */
+  verifySync(sets) {
+    const t0 = Date.now();
+    const res = addon.verifyJobsSync(this.syncEngine, ...packJobs([normalizeSets(sets, this.decompress)]));
+    const dt = Date.now() - t0;
+    this.stats.mainThreadMs += dt;
+    if (this.metrics) this.metrics.blsThreadPool.mainThreadDurationInThreadPool.observe(dt / 1000);
+    return codeToResult(res[0]);
   }
 
   /**
@@ -191,8 +286,7 @@ class BlsGpuVerifier {
    * @returns {boolean}
    */
   verifySignatureSet(set) {
-    validateSets([set]);
-    return codeToResult(addon.verifyJobsSync(this.engines[0], ...packJobs([[set]]))[0]);
+    return this.verifySync([set]);
   }
 
   /**
@@ -209,7 +303,7 @@ class BlsGpuVerifier {
       if (sg.length === 96) flat.set(sg, 96 * i);
       else odd = true;
     });
-    const r = addon.aggregateSignatures(this.engines[0], Uint32Array.from([0, signatures.length]), flat,
+    const r = addon.aggregateSignatures(this.syncEngine, Uint32Array.from([0, signatures.length]), flat,
       odd ? sizes : null, validate === undefined ? true : Boolean(validate));
     if (r.status[0] !== 0) throw Error(addon.errorName(r.status[0]));
     return r.out;
@@ -225,12 +319,10 @@ class BlsGpuVerifier {
     // costs one promise instead of four (the per-call promise machinery dominated the JS side)
     opts = opts || {};
     try {
-      if (this.closed) throw new QueueError("QUEUE_ABORTED");
-      validateSets(sets);
-      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
-        const res = addon.verifyJobsSync(this.engines[0], ...packJobs([sets]));
-        return Promise.resolve(codeToResult(res[0]));
-      }
+      if (this.closed) throw new QueueError({code: QueueErrorCode.QUEUE_ABORTED});
+      if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
+      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) return Promise.resolve(this.verifySync(sets));
+      sets = normalizeSets(sets, this.decompress);
     } catch (e) {
       return Promise.reject(e);
     }
@@ -244,20 +336,23 @@ class BlsGpuVerifier {
   async close() {
     this.closed = true;
     if (this.buffered) {
+      // (the reference only clears the timer and leaves these promises pending forever,
+      // multithread/index.ts:176-180; here they reject like the queued jobs)
       clearTimeout(this.buffered.timeout);
-      for (const job of this.buffered.jobs) job.reject(new QueueError("QUEUE_ABORTED"));
+      for (const job of this.buffered.jobs) job.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
       this.buffered = null;
     }
-    for (const job of this.jobs.splice(0)) job.reject(new QueueError("QUEUE_ABORTED"));
+    for (const job of this.jobs.splice(0)) job.reject(new QueueError({code: QueueErrorCode.QUEUE_ABORTED}));
     await Promise.all([...this.running]);
-    for (const e of this.engines) addon.destroyEngine(e);
+    for (const e of this.allEngines()) addon.destroyEngine(e);
     this.engines = [];
+    this.syncEngine = null;
     this.idle = [];
   }
 
   queueJob(sets, opts) {
     return new Promise((resolve, reject) => {
-      const job = {sets, resolve, reject};
+      const job = {sets, resolve, reject, addedTimeMs: Date.now()};
       if (opts.batchable) {
         if (!this.buffered) {
           this.buffered = {jobs: [], sigCount: 0, timeout: setTimeout(() => this.flushBuffer(), MAX_BUFFER_WAIT_MS)};
@@ -269,6 +364,7 @@ class BlsGpuVerifier {
         this.jobs.push(job);
         setTimeout(() => this.runJobs(), 0);
       }
+      if (this.metrics) this.metrics.blsThreadPool.queueLength.set(this.jobs.length);
     });
   }
 
@@ -299,27 +395,73 @@ class BlsGpuVerifier {
   }
 
   async runPackage(engine, pkg) {
+    const m = this.metrics;
+    const start = Date.now();
+    let startedSigSets = 0;
+    for (const j of pkg) {
+      const wait = start - j.addedTimeMs;
+      this.stats.jobWaitMs += wait;
+      if (m) m.blsThreadPool.jobWaitTime.observe(wait / 1000);
+      startedSigSets += j.sets.length;
+    }
+    if (m) {
+      m.blsThreadPool.totalJobsGroupsStarted.inc(1);
+      m.blsThreadPool.totalJobsStarted.inc(pkg.length);
+      m.blsThreadPool.totalSigSetsStarted.inc(startedSigSets);
+    }
     let codes;
     try {
       codes = await addon.verifyJobs(engine, ...packJobs(pkg.map((j) => j.sets)));
     } catch (e) {
       // device failure: every job of the package rejects (multithread/index.ts:368-375)
+      if (!this.closed && this.logger) this.logger.error("BlsGpuVerifier error", {}, e);
       for (const j of pkg) j.reject(e);
       return;
     }
+    const sec = (Date.now() - start) / 1000;
+    this.stats.deviceMs += sec * 1000;
     this.stats.batches++;
     this.stats.jobs += pkg.length;
+    let success = 0;
+    let error = 0;
+    let failed = false;
     pkg.forEach((j, k) => {
       this.stats.sets += j.sets.length;
       if (codes[k] < 0) {
         this.stats.jobsError++;
+        error += j.sets.length;
         j.reject(Error(addon.errorName(-codes[k])));
       } else {
-        if (codes[k] === 0) this.stats.jobsInvalid++;
+        if (codes[k] === 0) {
+          this.stats.jobsInvalid++;
+          failed = true;
+        }
+        success += j.sets.length;
         j.resolve(codes[k] === 1);
       }
     });
+    // a package with a false job failed its batch equation and ran the invalid-set search (the
+    // reference's batch retry, worker.ts:76-98); otherwise every live set was batch-verified
+    const retries = failed ? 1 : 0;
+    const batchSigs = failed ? 0 : success;
+    this.stats.batchRetries += retries;
+    this.stats.batchSigsSuccess += batchSigs;
+    if (m) {
+      m.blsThreadPool.timePerSigSet.observe(startedSigSets ? sec / startedSigSets : 0);
+      m.blsThreadPool.jobsWorkerTime.inc({workerId: this.engines.indexOf(engine)}, sec);
+      m.blsThreadPool.successJobsSignatureSetsCount.inc(success);
+      m.blsThreadPool.errorJobsSignatureSetsCount.inc(error);
+      m.blsThreadPool.batchRetries.inc(retries);
+      m.blsThreadPool.batchSigsSuccess.inc(batchSigs);
+    }
   }
+}
+
+/** chain/bls/utils.ts:18-26 */
+function getAggregatedPubkeysCount(sets) {
+  let n = 0;
+  for (const s of sets) if (s.type === SignatureSetType.aggregate) n += s.pubkeys.length;
+  return n;
 }
 
 /**
@@ -343,7 +485,11 @@ module.exports = {
   isValidBlsAggregate,
   GpuPublicKey,
   QueueError,
+  QueueErrorCode,
+  PointFormat,
   SignatureSetType,
+  normalizeSets,
+  getAggregatedPubkeysCount,
   chunkifyMaximizeChunkSize,
   packJobs,
   addon,

@@ -188,9 +188,13 @@ function aggregate(blobs, commitments) {
   }
   return {agg, rPowers, x};
 }
+// compressed point at infinity: the proof of zero blobs (the zero polynomial)
+const G1_INFINITY48 = Uint8Array.from([0xc0, ...new Array(47).fill(0)]);
+
 function computeAggregateKzgProof(blobs) {
   requireSetup();
-  if (!blobs.length) throw Error("computeAggregateKzgProof: no blobs");
+  // chain.ts:402 calls this for every produced block, blobless ones included
+  if (!blobs.length) return G1_INFINITY48.slice();
   const commitments = blobs.map(blobToKzgCommitment);
   const {agg, x} = aggregate(blobs, commitments);
   return commitCoefficients(quotient(evaluationsToCoefficients(agg), x));
@@ -198,7 +202,11 @@ function computeAggregateKzgProof(blobs) {
 function verifyAggregateKzgProof(blobs, expectedKzgCommitments, kzgAggregatedProof) {
   requireSetup();
   if (blobs.length !== expectedKzgCommitments.length) throw Error("blobs / commitments length mismatch");
-  if (!blobs.length) throw Error("verifyAggregateKzgProof: no blobs");
+  if (!blobs.length) {
+    // aggregated commitment = infinity, y = 0: true iff the proof is infinity (still decoded)
+    const {x} = computeChallenges([], []);
+    return addon.kzgVerifyProof(engine, G1_INFINITY48, bigToBytes(x, 32, true), bigToBytes(0n, 32, true), kzgAggregatedProof);
+  }
   const {agg, rPowers, x} = aggregate(blobs, expectedKzgCommitments);
   const pts = new Uint8Array(48 * expectedKzgCommitments.length);
   expectedKzgCommitments.forEach((c, i) => pts.set(c, 48 * i));
@@ -212,6 +220,7 @@ module.exports = {
   blobToKzgCommitment,
   computeAggregateKzgProof,
   verifyAggregateKzgProof,
+  G1_INFINITY48,
   // host field work, exported for tests
   _internal: {evaluationsToCoefficients, evaluate, quotient, computeChallenges, ROOTS, BRP, R},
 };

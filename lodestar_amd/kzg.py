@@ -166,6 +166,9 @@ def _scalars_le(vals: Sequence[int]) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ GPU-backed KZG
+G1_INFINITY48 = b"\xc0" + b"\x00" * 47  # compressed point at infinity
+
+
 class KzgError(Exception):
     pass
 
@@ -230,8 +233,11 @@ class Kzg:
         return self.commit_coefficients(quotient_coefficients(coeffs, z)), evaluate_coefficients(coeffs, z)
 
     def compute_aggregate_kzg_proof(self, blobs: Sequence[bytes]) -> bytes:
+        """c-kzg compute_aggregate_kzg_proof; called for every produced block (chain.ts:402), blobless
+        ones included: zero blobs aggregate to the zero polynomial, whose proof is the point at
+        infinity (the spec's compute_kzg_proof of the zero polynomial)."""
         if not blobs:
-            raise KzgError("computeAggregateKzgProof: no blobs")
+            return G1_INFINITY48
         commitments = [self.blob_to_kzg_commitment(b) for b in blobs]
         agg, _, x = self._aggregate(blobs, commitments)
         proof, _ = self.compute_kzg_proof_coefficients(evaluations_to_coefficients(agg), x)
@@ -257,7 +263,9 @@ class Kzg:
         if len(blobs) != len(commitments):
             raise KzgError("verifyAggregateKzgProof: blobs / commitments length mismatch")
         if not blobs:
-            raise KzgError("verifyAggregateKzgProof: no blobs")
+            # aggregated commitment = infinity, y = 0: e(pi, [tau - z] G2) == 1 iff pi is infinity
+            # (the check still decodes pi: a malformed proof raises)
+            return self.verify_kzg_proof(G1_INFINITY48, compute_challenges([], [])[1], 0, proof)
         agg, r_powers, x = self._aggregate(blobs, commitments)
         c = self.g1_lincomb(r_powers, list(commitments))
         y = evaluate_coefficients(evaluations_to_coefficients(agg), x)

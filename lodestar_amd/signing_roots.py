@@ -277,12 +277,17 @@ class StateView:
     fork_previous_version: bytes
     fork_current_version: bytes
     fork_epoch: int
-    genesis_fork_version: bytes
     pubkey: Callable[[int], object]                     # index2pubkey (epochContext.index2pubkey)
     beacon_committee: Callable[[int, int], List[int]]   # epochContext.getBeaconCommittee(slot, index)
     sync_committee: Callable[[], List[object]]          # current sync committee pubkeys (512)
+    slot: Optional[int] = None                          # state.slot (None: the block's slot)
+    # bls.PublicKey.fromBytes(bytes48, affine, true) for keys carried in the block itself
+    # (BLS-to-execution changes, blsToExecutionChange.ts:30)
+    key_from_bytes: Callable[[bytes], object] = lambda b: b
 
     def domain(self, domain_type: bytes, epoch: int) -> bytes:
+        """config.getDomain(state.slot, type, messageSlot) (config/src/genesisConfig/index.ts:27-54):
+        the state's previous fork version for messages before its fork epoch, else the current one"""
         v = self.fork_previous_version if epoch < self.fork_epoch else self.fork_current_version
         return compute_domain(domain_type, v, self.genesis_validators_root)
 
@@ -298,31 +303,34 @@ class BlockSet:
 
 def block_signature_sets(signed_block, state: StateView, skip_proposer_signature: bool = False) -> List[BlockSet]:
     """getBlockSignatureSets (signatureSets/index.ts:64-111) for one capella SignedBeaconBlock
-    (JSON as served by the beacon API).  Signing roots are left as trees: evaluate() hashes the
-    trees of many blocks together."""
+    (JSON as served by the beacon API), in the reference's order: randao, proposer slashings,
+    attester slashings, attestations, voluntary exits, proposer, sync aggregate, BLS-to-execution
+    changes.  Signing roots are left as trees: evaluate() hashes the trees of many blocks together."""
     m = signed_block["message"]
     b = m["body"]
     slot = int(m["slot"])
     epoch = slot // SLOTS_PER_EPOCH
+    state_epoch = (slot if state.slot is None else int(state.slot)) // SLOTS_PER_EPOCH
     out: List[BlockSet] = []
-    if not skip_proposer_signature:
-        out.append(BlockSet("proposer", "single", [state.pubkey(int(m["proposer_index"]))],
-                            signing_tree(beacon_block_capella(m), state.domain(DOMAIN_BEACON_PROPOSER, epoch)),
-                            hx(signed_block["signature"])))
+    # randao.ts:26
     out.append(BlockSet("randao", "single", [state.pubkey(int(m["proposer_index"]))],
                         signing_tree(uint64(epoch), state.domain(DOMAIN_RANDAO, epoch)), hx(b["randao_reveal"])))
+    # proposerSlashings.ts:14-37: both headers are checked against signedHeader1's proposer
     for s in b["proposer_slashings"]:
+        pk = state.pubkey(int(s["signed_header_1"]["message"]["proposer_index"]))
         for h in (s["signed_header_1"], s["signed_header_2"]):
             ep = int(h["message"]["slot"]) // SLOTS_PER_EPOCH
-            out.append(BlockSet("proposer_slashing", "single", [state.pubkey(int(h["message"]["proposer_index"]))],
+            out.append(BlockSet("proposer_slashing", "single", [pk],
                                 signing_tree(block_header(h["message"]), state.domain(DOMAIN_BEACON_PROPOSER, ep)),
                                 hx(h["signature"])))
+    # attesterSlashings.ts:32
     for s in b["attester_slashings"]:
         for ia in (s["attestation_1"], s["attestation_2"]):
             ep = int(ia["data"]["target"]["epoch"])
             out.append(BlockSet("attester_slashing", "aggregate", [state.pubkey(int(i)) for i in ia["attesting_indices"]],
                                 signing_tree(attestation_data(ia["data"]), state.domain(DOMAIN_BEACON_ATTESTER, ep)),
                                 hx(ia["signature"])))
+    # indexedAttestation.ts:6-37
     for a in b["attestations"]:
         d = a["data"]
         committee = state.beacon_committee(int(d["slot"]), int(d["index"]))
@@ -332,11 +340,18 @@ def block_signature_sets(signed_block, state: StateView, skip_proposer_signature
                             signing_tree(attestation_data(d), state.domain(DOMAIN_BEACON_ATTESTER,
                                                                            int(d["target"]["epoch"]))),
                             hx(a["signature"])))
+    # voluntaryExits.ts:28
     for e in b["voluntary_exits"]:
         out.append(BlockSet("voluntary_exit", "single", [state.pubkey(int(e["message"]["validator_index"]))],
                             signing_tree(voluntary_exit(e["message"]),
                                          state.domain(DOMAIN_VOLUNTARY_EXIT, int(e["message"]["epoch"]))),
                             hx(e["signature"])))
+    # proposer.ts:20 (index.ts:86-88: after the operations)
+    if not skip_proposer_signature:
+        out.append(BlockSet("proposer", "single", [state.pubkey(int(m["proposer_index"]))],
+                            signing_tree(beacon_block_capella(m), state.domain(DOMAIN_BEACON_PROPOSER, epoch)),
+                            hx(signed_block["signature"])))
+    # block/processSyncCommittee.ts:58-111
     sa = b["sync_aggregate"]
     bits = bits_from_bitvector_hex(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)
     keys = [k for k, bit in zip(state.sync_committee(), bits) if bit]
@@ -346,9 +361,11 @@ def block_signature_sets(signed_block, state: StateView, skip_proposer_signature
                             signing_tree(hx(m["parent_root"]), state.domain(DOMAIN_SYNC_COMMITTEE,
                                                                             prev // SLOTS_PER_EPOCH)),
                             hx(sa["sync_committee_signature"])))
+    # blsToExecutionChange.ts:23: getDomain(state.slot, DOMAIN_BLS_TO_EXECUTION_CHANGE), i.e. the
+    # fork of the state's own epoch; the key is the message's from_bls_pubkey (48 B compressed)
     for c in b["bls_to_execution_changes"]:
-        dom = compute_domain(DOMAIN_BLS_TO_EXECUTION_CHANGE, state.genesis_fork_version, state.genesis_validators_root)
-        out.append(BlockSet("bls_to_execution_change", "single", [c["message"]["from_bls_pubkey"]],
+        dom = state.domain(DOMAIN_BLS_TO_EXECUTION_CHANGE, state_epoch)
+        out.append(BlockSet("bls_to_execution_change", "single", [state.key_from_bytes(hx(c["message"]["from_bls_pubkey"]))],
                             signing_tree(bls_to_execution_change(c["message"]), dom), hx(c["signature"])))
     return out
 

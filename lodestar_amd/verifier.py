@@ -7,7 +7,7 @@ Reference interface and policy (paths under the reference repo):
       - batchable jobs buffered until >32 sigs or 100 ms (:48,57,257-275)
       - non-batchable jobs run on the next tick (:280-283)
       - verifyOnMainThread runs synchronously on the caller's thread (:138-151)
-      - close() rejects queued jobs with QUEUE_ABORTED (:176-197)
+      - close() rejects queued jobs with QueueError(QUEUE_ABORTED) (:176-197)
   * per-job results (worker.ts:32-108): job j resolves true/false or rejects with its error,
     independently of every other job in the same batch (multithread.test.ts:86-103).
 
@@ -34,12 +34,20 @@ MAX_BUFFERED_SIGS = 32             # multithread/index.ts:48
 MAX_BUFFER_WAIT_MS = 100           # multithread/index.ts:57
 
 
-class QueueError(Exception):
-    """util/queue QueueError; code QUEUE_ABORTED after close()."""
+class QueueErrorCode(str, Enum):
+    """beacon-node/src/util/queue/errors.ts:3-6"""
+    QUEUE_ABORTED = "QUEUE_ERROR_QUEUE_ABORTED"
+    QUEUE_MAX_LENGTH = "QUEUE_ERROR_QUEUE_MAX_LENGTH"
 
-    def __init__(self, code: str = "QUEUE_ABORTED"):
-        self.code = code
-        super().__init__(code)
+
+class QueueError(Exception):
+    """util/queue QueueError (a LodestarError: `type` = {code}, message = type.code,
+    utils/src/errors.ts:6-8); code QUEUE_ABORTED after close()."""
+
+    def __init__(self, type_: Optional[dict] = None):
+        self.type = dict(type_ or {"code": QueueErrorCode.QUEUE_ABORTED.value})
+        self.code = self.type["code"]
+        super().__init__(self.code)
 
 
 def chunkify_maximize_chunk_size(arr: Sequence, min_per_chunk: int) -> List[list]:
@@ -166,7 +174,10 @@ class BlsGpuVerifier:
                 raise ValueError("n_engines must be >= 1")
             self.engines = [Engine(device) for _ in range(n_engines)]
             self._own_engines = True
-        self.engine = self.engines[0]
+        # synchronous callers (verify_on_main_thread, verify_signature_set, aggregate_signatures,
+        # key decompression) use an engine outside the runners' pool when the pool owns its
+        # engines, so they never wait behind a batch in flight (multithread/index.ts:138-151)
+        self.engine = Engine(device) if self._own_engines else self.engines[0]
         self.bls_verify_all_multi_thread = bls_verify_all_multi_thread
         self.stats = PoolStats()
         self._lock = threading.Condition()
@@ -185,7 +196,7 @@ class BlsGpuVerifier:
                                     opts: Optional[VerifySignatureOpts] = None) -> bool:
         opts = opts or VerifySignatureOpts()
         if self._closed:
-            raise QueueError("QUEUE_ABORTED")
+            raise QueueError({"code": QueueErrorCode.QUEUE_ABORTED.value})
         inputs = [_to_input(s) for s in sets]
         idx = []
         for s in sets:
@@ -216,11 +227,11 @@ class BlsGpuVerifier:
             self._jobs, self._buffered, self._buffered_sigs = [], [], 0
             self._lock.notify_all()
         for j in pending:
-            j.loop.call_soon_threadsafe(_set_exc, j.future, QueueError("QUEUE_ABORTED"))
+            j.loop.call_soon_threadsafe(_set_exc, j.future, QueueError({"code": QueueErrorCode.QUEUE_ABORTED.value}))
         for t in self._runners:
             await asyncio.get_running_loop().run_in_executor(None, t.join)
         if self._own_engines:
-            for e in self.engines:
+            for e in [self.engine] + self.engines:
                 e.close()
 
     # ---------------------------------------------------------------- direct (non-pool) callers
@@ -250,7 +261,8 @@ class BlsGpuVerifier:
         else:
             raws = pks
         first = None
-        for e in self.engines:  # every engine holds the same table (same indices)
+        engines = self.engines if self.engine in self.engines else [self.engine] + self.engines
+        for e in engines:  # every engine holds the same table (same indices)
             f, st = e.pubkey_table_append(raws, validate)
             for s in st:
                 if s:

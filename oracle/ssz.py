@@ -29,7 +29,9 @@ FAR_FUTURE_EPOCH = 2 ** 64 - 1
 DOMAIN_BEACON_PROPOSER = bytes.fromhex("00000000")
 DOMAIN_BEACON_ATTESTER = bytes.fromhex("01000000")
 DOMAIN_RANDAO = bytes.fromhex("02000000")
+DOMAIN_VOLUNTARY_EXIT = bytes.fromhex("04000000")
 DOMAIN_SYNC_COMMITTEE = bytes.fromhex("07000000")
+DOMAIN_BLS_TO_EXECUTION_CHANGE = bytes.fromhex("0a000000")
 
 ZERO = bytes(32)
 
@@ -160,18 +162,44 @@ def execution_payload_capella(p) -> bytes:
         list_of(txs, 2 ** 20), list_of([withdrawal(w) for w in p["withdrawals"]], 16)])
 
 
+def block_header(h) -> bytes:
+    """phase0 BeaconBlockHeader"""
+    return container([uint64(int(h["slot"])), uint64(int(h["proposer_index"])), hx(h["parent_root"]),
+                      hx(h["state_root"]), hx(h["body_root"])])
+
+
+def signed_block_header(s) -> bytes:
+    return container([block_header(s["message"]), bytes_n(hx(s["signature"]))])
+
+
+def voluntary_exit(e) -> bytes:
+    return container([uint64(int(e["epoch"])), uint64(int(e["validator_index"]))])
+
+
+def bls_to_execution_change(c) -> bytes:
+    """capella BLSToExecutionChange"""
+    return container([uint64(int(c["validator_index"])), bytes_n(hx(c["from_bls_pubkey"])),
+                      bytes_n(hx(c["to_execution_address"]))])
+
+
 def beacon_block_body_capella(b) -> bytes:
-    for k in ("proposer_slashings", "attester_slashings", "deposits", "voluntary_exits", "bls_to_execution_changes"):
+    for k in ("attester_slashings", "deposits"):
         if b[k]:
-            raise NotImplementedError(f"{k} present in the block: not needed by the K3 fixture")
+            raise NotImplementedError(f"{k} present in the block: not needed by the fixtures")
     sa = b["sync_aggregate"]
     return container([
         bytes_n(hx(b["randao_reveal"])), eth1_data(b["eth1_data"]), hx(b["graffiti"]),
-        list_of([], 16), list_of([], 2), list_of([attestation(a) for a in b["attestations"]], 128),
-        list_of([], 16), list_of([], 16),
+        list_of([container([signed_block_header(s["signed_header_1"]), signed_block_header(s["signed_header_2"])])
+                 for s in b["proposer_slashings"]], 16),
+        list_of([], 2), list_of([attestation(a) for a in b["attestations"]], 128),
+        list_of([], 16),
+        list_of([container([voluntary_exit(e["message"]), bytes_n(hx(e["signature"]))])
+                 for e in b["voluntary_exits"]], 16),
         container([bitvector(bits_from_hex_bitvector(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)),
                    bytes_n(hx(sa["sync_committee_signature"]))]),
-        execution_payload_capella(b["execution_payload"]), list_of([], 16)])
+        execution_payload_capella(b["execution_payload"]),
+        list_of([container([bls_to_execution_change(c["message"]), bytes_n(hx(c["signature"]))])
+                 for c in b["bls_to_execution_changes"]], 16)])
 
 
 def beacon_block_capella(m) -> bytes:

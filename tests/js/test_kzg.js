@@ -43,6 +43,11 @@ if (mode === "cpu") {
   bad[31] ^= 1;
   assert.strictEqual(kzg.verifyAggregateKzgProof([blobs[0], bad], comms, proof), false);
   assert.strictEqual(kzg.verifyAggregateKzgProof(blobs, comms.slice().reverse(), proof), false);
+  // zero blobs (a blobless block, chain.ts:402): the proof is the point at infinity
+  const inf = kzg.computeAggregateKzgProof([]);
+  assert.strictEqual(hex(inf), "c0" + "00".repeat(47));
+  assert.strictEqual(kzg.verifyAggregateKzgProof([], [], inf), true);
+  assert.strictEqual(kzg.verifyAggregateKzgProof([], [], proof), false);
   console.log(JSON.stringify({commitments: comms.map(hex), proof: hex(proof)}));
   console.log("js kzg gpu ok");
 }

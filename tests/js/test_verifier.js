@@ -26,6 +26,40 @@ function cpuTests() {
   const set = {type: "single", pubkey: new Uint8Array(96), signingRoot: new Uint8Array(32), signature: new Uint8Array(32)};
   const packed = m.packJobs([[set]]);
   assert.strictEqual(packed[5][0], 32);
+  // QueueError as beacon-node/src/util/queue/errors.ts:3-14 (message = type.code)
+  const qe = new m.QueueError({code: m.QueueErrorCode.QUEUE_ABORTED});
+  assert.strictEqual(qe.type.code, "QUEUE_ERROR_QUEUE_ABORTED");
+  assert.strictEqual(qe.message, "QUEUE_ERROR_QUEUE_ABORTED");
+  // @chainsafe/bls PublicKey objects: toBytes(PointFormat.uncompressed) is what gets shipped; a key
+  // whose toBytes ignores the format (48-byte default) is decompressed in one batch per call
+  const b96 = Uint8Array.from({length: 96}, (_, i) => i);
+  const b48 = Uint8Array.from({length: 48}, (_, i) => 200 - i);
+  const formats = [];
+  const pkU = {toBytes: (f) => (formats.push(f), f === "uncompressed" ? b96 : b48)};
+  const pkC = {toBytes: () => b48};
+  const calls = [];
+  const stub = (flat) => {
+    calls.push(flat.length);
+    return {out: new Uint8Array(2 * flat.length).fill(7), status: new Int32Array(flat.length / 48)};
+  };
+  const sets = [
+    {type: "single", pubkey: pkU, signingRoot: new Uint8Array(32), signature: new Uint8Array(96)},
+    {type: "aggregate", pubkeys: [pkC, pkU, b48], signingRoot: new Uint8Array(32), signature: new Uint8Array(96)},
+  ];
+  const norm = m.normalizeSets(sets, stub);
+  assert.deepStrictEqual(calls, [96]);  // pkC + the raw 48-byte key, one batch
+  assert.strictEqual(formats[0], "uncompressed");
+  assert.strictEqual(norm[0], sets[0]);  // untouched: its key is already 96 bytes
+  assert.strictEqual(norm[1].pubkeys[0][0], 7);
+  assert.strictEqual(norm[1].pubkeys[1], pkU);
+  assert.strictEqual(sets[1].pubkeys[0], pkC);  // the caller's sets are not modified
+  m.normalizeSets(sets, stub);  // the key objects' 96-byte forms are cached
+  assert.deepStrictEqual(calls, [96, 48]);
+  assert.strictEqual(formats.length, 1);
+  assert.throws(() => m.normalizeSets([{...sets[0], pubkey: {toBytes: () => new Uint8Array(47)}}], stub), /48 or 96/);
+  assert.throws(() => m.normalizeSets([{...sets[1], pubkeys: [b48]}],
+    (flat) => ({out: new Uint8Array(96), status: Int32Array.from([1])})), /BLST_BAD_ENCODING/);
+  assert.strictEqual(m.getAggregatedPubkeysCount(sets), 3);
   console.log("js cpu ok");
 }
 
@@ -35,6 +69,36 @@ function setsFromCase(c) {
       ? {type: "single", pubkey: hex(s.pubkeys[0]), signingRoot: hex(s.signing_root), signature: hex(s.signature)}
       : {type: "aggregate", pubkeys: s.pubkeys.map(hex), signingRoot: hex(s.signing_root), signature: hex(s.signature)}
   );
+}
+
+// a @chainsafe/bls-shaped PublicKey: toBytes() defaults to the 48-byte compressed encoding
+// (PointFormat.compressed); toBytes("uncompressed") gives the 96 bytes the reference pool ships
+const P_FIELD = BigInt("0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab");
+function compress96(b96) {
+  const out = Uint8Array.from(b96.subarray(0, 48));
+  if (b96[0] & 0x40) {
+    out.fill(0);
+    out[0] = 0xc0;
+    return out;
+  }
+  const y = BigInt("0x" + Buffer.from(b96.subarray(48, 96)).toString("hex"));
+  out[0] |= 0x80 | (2n * y > P_FIELD ? 0x20 : 0);
+  return out;
+}
+class MockPublicKey {
+  constructor(b96, ignoreFormat) {
+    this.b96 = b96;
+    this.b48 = compress96(b96);
+    this.ignoreFormat = ignoreFormat;
+  }
+  toBytes(format) {
+    return format === "uncompressed" && !this.ignoreFormat ? this.b96 : this.b48;
+  }
+}
+function mockSets(c, ignoreFormat) {
+  return setsFromCase(c).map((s) =>
+    s.type === "single" ? {...s, pubkey: new MockPublicKey(s.pubkey, ignoreFormat)}
+      : {...s, pubkeys: s.pubkeys.map((k) => new MockPublicKey(k, ignoreFormat))});
 }
 
 async function outcome(p) {
@@ -52,6 +116,19 @@ async function gpuTests() {
   for (const batchable of [false, true]) {
     const got = await Promise.all(cases.map((c) => outcome(pool.verifySignatureSets(setsFromCase(c), {batchable}))));
     cases.forEach((c, k) => assert.strictEqual(got[k], c.expected, `${c.name} batchable=${batchable}`));
+  }
+  // the reference's own key objects (@chainsafe/bls PublicKey): serialised with
+  // toBytes("uncompressed"), or decompressed on the GPU when toBytes only gives 48 bytes.  Keys that
+  // do not decode cannot exist as PublicKey objects (pubkey_* cases are byte-level only).
+  const keyCases = cases.filter((c) => !c.name.startsWith("pubkey_"));
+  for (const ignoreFormat of [false, true]) {
+    for (const batchable of [false, true]) {
+      const got = await Promise.all(keyCases.map((c) => outcome(pool.verifySignatureSets(mockSets(c, ignoreFormat), {batchable}))));
+      keyCases.forEach((c, k) => assert.strictEqual(got[k], c.expected, `${c.name} mock keys ignoreFormat=${ignoreFormat}`));
+    }
+    for (const c of keyCases.slice(0, 12))
+      assert.strictEqual(await outcome(pool.verifySignatureSets(mockSets(c, ignoreFormat), {verifyOnMainThread: true})),
+        c.expected, `${c.name} main thread mock keys`);
   }
   // verifyOnMainThread path
   for (const c of cases.slice(0, 10)) {
@@ -133,10 +210,23 @@ async function gpuTests() {
     if (g.status === "BLST_SUCCESS") assert.strictEqual(Buffer.from(pool.aggregateSignatures(sigs)).toString("hex"), g.expected96);
     else assert.throws(() => pool.aggregateSignatures(sigs), new RegExp(g.status));
   }
-  // close(): queued jobs abort
-  const pending = outcome(pool.verifySignatureSets(k4, {batchable: true}));
+  // verifyOnMainThread runs on its own engine: it does not wait for a pool batch in flight
+  const big = [];
+  for (let r = 0; r < 40; r++) big.push(...k4);
+  const inflightBatch = pool.verifySignatureSets(big);
+  assert.strictEqual(pool.verifySignatureSets([k4[0]], {verifyOnMainThread: true}) instanceof Promise, true);
+  assert.strictEqual(await inflightBatch, true);
+  assert.ok(pool.stats.batchRetries >= 1);  // the false / rejected golden jobs above
+  // close(): queued jobs abort with QueueError(QUEUE_ABORTED) (util/queue/errors.ts:3-6)
+  const pendingP = pool.verifySignatureSets(k4, {batchable: true});
+  let qerr = null;
+  pendingP.catch((e) => { qerr = e; });
   await pool.close();
-  assert.strictEqual(await pending, "QUEUE_ABORTED");
+  await pendingP.catch(() => {});
+  assert.ok(qerr instanceof m.QueueError);
+  assert.strictEqual(qerr.type.code, m.QueueErrorCode.QUEUE_ABORTED);
+  assert.strictEqual(qerr.message, "QUEUE_ERROR_QUEUE_ABORTED");
+  await assert.rejects(pool.verifySignatureSets(k4), (e) => e.type.code === "QUEUE_ERROR_QUEUE_ABORTED");
   console.log("js gpu ok");
 }
 

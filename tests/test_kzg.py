@@ -116,5 +116,35 @@ def test_aggregate_proof_round_trip_and_tampering(kzg):
     assert kzg.verifyAggregateKzgProof(blobs, comms, kzg.computeAggregateKzgProof(blobs[:1])) is False
     # one blob
     assert kzg.verifyAggregateKzgProof(blobs[:1], comms[:1], kzg.computeAggregateKzgProof(blobs[:1])) is True
+    # zero blobs (every blobless block, chain.ts:402): the proof is the point at infinity and
+    # verifies against no commitments; any other proof does not
+    inf = bytes([0xC0]) + bytes(47)
+    assert kzg.computeAggregateKzgProof([]) == inf
+    assert kzg.verifyAggregateKzgProof([], [], inf) is True
+    assert kzg.verifyAggregateKzgProof([], [], proof) is False
     with pytest.raises(K.KzgError):
-        kzg.verifyAggregateKzgProof([], [], proof)
+        kzg.verifyAggregateKzgProof(blobs[:1], [], proof)
+
+
+def _off_subgroup_g1():
+    """an on-curve G1 point outside the order-r subgroup (cofactor component)"""
+    x = 5
+    while True:
+        y = o.fp_sqrt((x * x * x + o.B1) % o.P)
+        if y is not None and o.g1_mul((x, y), R) is not None:
+            return (x, y)
+        x += 1
+
+
+@pytest.mark.gpu
+def test_points_outside_g1_are_rejected(kzg):
+    """c-kzg validate_kzg_g1: commitments, proofs and lincomb points must lie in G1"""
+    bad = o.g1_compress(_off_subgroup_g1())
+    good = o.g1_compress(o.G1)
+    with pytest.raises(K.KzgError, match="BLST_POINT_NOT_IN_GROUP"):
+        kzg.g1_lincomb([1, 2], [good, bad])
+    with pytest.raises(K.KzgError, match="BLST_POINT_NOT_IN_GROUP"):
+        kzg.verify_kzg_proof(bad, 3, 4, good)
+    with pytest.raises(K.KzgError, match="BLST_POINT_NOT_IN_GROUP"):
+        kzg.verify_kzg_proof(good, 3, 4, bad)
+    assert kzg.verify_kzg_proof(good, 3, 4, good) is False  # in-group points still decide normally

@@ -99,8 +99,11 @@ def test_close_aborts_queued():
         fut = asyncio.ensure_future(pool.verify_signature_sets(mk_sets(1), V.VerifySignatureOpts(batchable=True)))
         await asyncio.sleep(0)
         await pool.close()
-        with pytest.raises(V.QueueError, match="QUEUE_ABORTED"):
+        with pytest.raises(V.QueueError, match="^QUEUE_ERROR_QUEUE_ABORTED$") as ei:
             await fut
-        with pytest.raises(V.QueueError):
+        # util/queue/errors.ts:3-6: callers compare e.type.code with QueueErrorCode.QUEUE_ABORTED
+        assert ei.value.type == {"code": V.QueueErrorCode.QUEUE_ABORTED.value} == {"code": "QUEUE_ERROR_QUEUE_ABORTED"}
+        with pytest.raises(V.QueueError) as ei:
             await pool.verify_signature_sets(mk_sets(1))
+        assert ei.value.type["code"] == "QUEUE_ERROR_QUEUE_ABORTED"
     run(main())

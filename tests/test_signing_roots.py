@@ -38,8 +38,8 @@ def k3_state(k3, pubkey=lambda b: b):
         genesis_validators_root=bytes.fromhex(k3["genesis_validators_root"]),
         fork_previous_version=bytes.fromhex(k3["fork"]["previous_version"]),
         fork_current_version=bytes.fromhex(k3["fork"]["current_version"]),
-        fork_epoch=k3["fork"]["epoch"], genesis_fork_version=bytes.fromhex(k3["fork"]["previous_version"]),
-        pubkey=lambda i: pubkey(keys[i]),
+        fork_epoch=k3["fork"]["epoch"],
+        pubkey=lambda i: pubkey(keys[i]), key_from_bytes=pubkey,
         beacon_committee=lambda slot, index: sv["committees"][f"{slot}:{index}"],
         sync_committee=lambda: [pubkey(keys[i]) for i in sv["sync_committee_indices"]])
 
@@ -47,9 +47,11 @@ def k3_state(k3, pubkey=lambda b: b):
 def test_k3_block_signing_roots_cpu_walk():
     k3 = load_json("k3_devnet.json")
     sets = SR.resolve(SR.block_signature_sets(k3["signed_block"], k3_state(k3)), cpu_merkleize)
-    gold = k3["sets"]
-    assert [s.name for s in sets] == ["proposer", "randao", "attestation", "sync_aggregate"]
-    for s, g in zip(sets, gold):
+    gold = {g["name"].split("_slot")[0]: g for g in k3["sets"]}
+    # getBlockSignatureSets order (signatureSets/index.ts:64-111)
+    assert [s.name for s in sets] == ["randao", "attestation", "proposer", "sync_aggregate"]
+    for s in sets:
+        g = gold[s.name]
         assert s.signing_root.hex() == g["signing_root"], s.name
         assert s.signature.hex() == g["signature"]
         assert len(s.pubkeys) == len(g["pubkeys"])
@@ -84,7 +86,8 @@ def test_k3_signing_roots_gpu_and_verify(engine):
             pk96[b48] = out[0]
         return pk96[b48]
     sets = SR.resolve(SR.block_signature_sets(k3["signed_block"], k3_state(k3, pub)), m)
-    assert [s.signing_root.hex() for s in sets] == [g["signing_root"] for g in k3["sets"]]
+    gold = {g["name"].split("_slot")[0]: g["signing_root"] for g in k3["sets"]}
+    assert [s.signing_root.hex() for s in sets] == [gold[s.name] for s in sets]
     assert m.launches <= 12  # one launch per tree level, however many trees
     block = SR.beacon_block_capella(k3["signed_block"]["message"])
     assert SR.evaluate([block], m)[0].hex() == k3["block_root"]
@@ -92,5 +95,78 @@ def test_k3_signing_roots_gpu_and_verify(engine):
     jobs = [[SetInput(s.pubkeys, s.signing_root, s.signature)] for s in sets]
     assert engine.verify_jobs(jobs) == [1, 1, 1, 1]
     assert engine.verify_jobs([[j[0] for j in jobs]]) == [1]
-    bad = SetInput(sets[3].pubkeys[1:], sets[3].signing_root, sets[3].signature)  # one participant short
+    sync = [s for s in sets if s.name == "sync_aggregate"][0]
+    bad = SetInput(sync.pubkeys[1:], sync.signing_root, sync.signature)  # one participant short
     assert engine.verify_jobs([[bad]]) == [0]
+
+
+def _operations_block(k3):
+    """The K3 block with operations the devnet block lacks: a proposer slashing whose two headers
+    name DIFFERENT proposers (the reference takes signedHeader1's key for both,
+    proposerSlashings.ts:14-16), a voluntary exit and a BLS-to-execution change.  Signatures are
+    placeholders: only the set list and its signing roots are compared."""
+    import copy
+    blk = copy.deepcopy(k3["signed_block"])
+    b = blk["message"]["body"]
+    slot = int(blk["message"]["slot"])
+
+    def header(pi, salt):
+        return {"message": {"slot": str(slot - 40), "proposer_index": str(pi), "parent_root": "0x" + salt * 32,
+                            "state_root": "0x" + "22" * 32, "body_root": "0x" + "33" * 32},
+                "signature": "0x" + salt * 96}
+    b["proposer_slashings"] = [{"signed_header_1": header(3, "a1"), "signed_header_2": header(5, "a2")}]
+    b["voluntary_exits"] = [{"message": {"epoch": "1", "validator_index": "7"}, "signature": "0x" + "b1" * 96}]
+    key48 = k3["state_view"]["validator_pubkeys48"][9]
+    b["bls_to_execution_changes"] = [{"message": {"validator_index": "9", "from_bls_pubkey": "0x" + key48,
+                                                  "to_execution_address": "0x" + "c1" * 20},
+                                      "signature": "0x" + "c2" * 96}]
+    return blk
+
+
+def test_operations_sets_match_oracle():
+    """order, keys and domains of the operation sets against oracle/ssz.py: the BLS
+    change's domain uses the state's fork (config.getDomain(state.slot, ..), blsToExecutionChange.ts:23),
+    not the genesis fork version; slashings use header 1's proposer for both sets"""
+    import oracle.ssz as S
+    k3 = load_json("k3_devnet.json")
+    blk = _operations_block(k3)
+    st = k3_state(k3)
+    sets = SR.resolve(SR.block_signature_sets(blk, st), cpu_merkleize)
+    assert [s.name for s in sets] == ["randao", "proposer_slashing", "proposer_slashing", "attestation",
+                                      "voluntary_exit", "proposer", "sync_aggregate", "bls_to_execution_change"]
+    keys = [bytes.fromhex(k) for k in k3["state_view"]["validator_pubkeys48"]]
+    m = blk["message"]
+    b = m["body"]
+    epoch = int(m["slot"]) // S.SLOTS_PER_EPOCH
+    gvr = bytes.fromhex(k3["genesis_validators_root"])
+    prev_v, cur_v = bytes.fromhex(k3["fork"]["previous_version"]), bytes.fromhex(k3["fork"]["current_version"])
+
+    def dom(t, ep):
+        return S.compute_domain(t, prev_v if ep < k3["fork"]["epoch"] else cur_v, gvr)
+    ps = b["proposer_slashings"][0]
+    exp = {
+        1: (keys[3], S.signing_root(S.block_header(ps["signed_header_1"]["message"]), dom(S.DOMAIN_BEACON_PROPOSER, epoch - 2))),
+        2: (keys[3], S.signing_root(S.block_header(ps["signed_header_2"]["message"]), dom(S.DOMAIN_BEACON_PROPOSER, epoch - 2))),
+        4: (keys[7], S.signing_root(S.voluntary_exit(b["voluntary_exits"][0]["message"]), dom(S.DOMAIN_VOLUNTARY_EXIT, 1))),
+        5: (keys[int(m["proposer_index"])], S.signing_root(S.beacon_block_capella(m), dom(S.DOMAIN_BEACON_PROPOSER, epoch))),
+        7: (keys[9], S.signing_root(S.bls_to_execution_change(b["bls_to_execution_changes"][0]["message"]),
+                                    dom(S.DOMAIN_BLS_TO_EXECUTION_CHANGE, epoch))),
+    }
+    for k, (key, root) in exp.items():
+        assert sets[k].pubkeys == [key], sets[k].name
+        assert sets[k].signing_root == root, sets[k].name
+    # the state's fork at this epoch is the current one, so the genesis-version domain would differ
+    assert epoch >= k3["fork"]["epoch"] and prev_v != cur_v
+    wrong = S.signing_root(S.bls_to_execution_change(b["bls_to_execution_changes"][0]["message"]),
+                           S.compute_domain(S.DOMAIN_BLS_TO_EXECUTION_CHANGE, prev_v, gvr))
+    assert sets[7].signing_root != wrong
+
+
+@pytest.mark.gpu
+def test_operations_sets_gpu_roots(engine):
+    """the same operations block through lb_merkleize: roots equal the hashlib walk's"""
+    k3 = load_json("k3_devnet.json")
+    blk = _operations_block(k3)
+    cpu = SR.resolve(SR.block_signature_sets(blk, k3_state(k3)), cpu_merkleize)
+    gpu = SR.resolve(SR.block_signature_sets(blk, k3_state(k3)), SR.GpuMerkleizer(engine))
+    assert [s.signing_root for s in gpu] == [s.signing_root for s in cpu]
