@@ -19,11 +19,19 @@ Secondary measurements on the same line (rank 0; N = 1 unless noted):
   value_one_batch_in_flight     one engine, the same batch
   value_distinct_roots          every signing root distinct (the no-sharing bound)
   value_one_invalid_per_batch   one wrong-message attestation per slot (the invalid-set search)
+  value_e2e                     the headline batches through lb_verify_jobs_indexed with the same
+                                engines in flight: inputs in pinned host memory, so the pinned
+                                upload (H2D), the host-side chunk decomposition, every kernel and
+                                the per-job readback are inside the timed region (SURVEY §8(d)'s
+                                metric definition without the JS ceiling)
   value_slots1                  one slot per batch, one batch in flight (+ its latency)
   latency_1set_ms / latency_block_ms   one 1-set call / one c2 block call through lb_verify_jobs
-  per_config                    c1, c2, c4, c5 at one batch in flight (resident, lb_batch_verify)
+  per_config                    c1, c2, c4, c5, c5_64 at one batch in flight (resident, lb_batch_verify)
   value_dropin                  c3 through the JS IBlsVerifier (tools/bench_dropin.js): JS
-                                marshalling + pinned copy + H2D inside the timed region
+                                marshalling + pinned copy + H2D inside the timed region (median of
+                                10 rounds; + verifyOnMainThread 1-set latency under load)
+  signing_roots                 getBlockSignatureSets + GPU merkleization from JS (K3 block,
+                                128-attestation block, 32-block segment)
   cpu_baseline / cpu_c1         the reference worker policy on host cores (oracle/cpu_pool.cpp)
 """
 import argparse
@@ -69,6 +77,7 @@ def parse():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (invalid-set, slots1, latencies, per-config, drop-in)")
     ap.add_argument("--dropin-engines", type=int, default=4)
+    ap.add_argument("--dropin-rounds", type=int, default=10, help="drop-in leg: timed rounds (median reported)")
     return ap.parse_args()
 
 
@@ -201,10 +210,72 @@ def profiled_stages(eng, fn):
     return {k: round(v, 3) for k, v in prof.items() if v > 0}
 
 
-def extra_legs(a, engs, barrier, W):
+def pinned_like(lib, arr, keep):
+    """a copy of `arr` in pinned host memory (lb_host_alloc); the allocation is appended to keep"""
+    import ctypes
+    arr = np.ascontiguousarray(arr)
+    n = max(arr.nbytes, 1)
+    p = lib.lb_host_alloc(n)
+    if not p:
+        raise MemoryError("lb_host_alloc")
+    keep.append(p)
+    buf = (ctypes.c_uint8 * n).from_address(p)
+    out = np.frombuffer(buf, dtype=arr.dtype, count=arr.size).reshape(arr.shape)
+    out[...] = arr
+    return out
+
+
+def e2e_leg(a, engs, barrier, W, wl):
+    """value_e2e: every engine uploads + verifies + reads back the headline batch from pinned host
+    memory (lb_verify_jobs_indexed through its engine-owned workspace), batches in flight."""
+    import threading
+    lib = engs[0].lib
+    keep = []
+    try:
+        packs = []
+        for e in engs:
+            ip = W.indexed_for(e, wl)
+            packs.append(W.PackedJobs(job_off=pinned_like(lib, ip.job_off, keep), pk_off=pinned_like(lib, ip.pk_off, keep),
+                                      pubkeys=None, msgs=pinned_like(lib, ip.msgs, keep),
+                                      sigs=pinned_like(lib, ip.sigs, keep), sig_sizes=None,
+                                      pk_indices=pinned_like(lib, ip.pk_indices, keep)))
+        for e, pk in zip(engs, packs):  # warm the workspaces
+            assert np.array_equal(np.asarray(e.verify_jobs_packed(pk)), wl.expected), "e2e verdicts differ"
+        steps = max(2, a.steps // 2)
+        res = [None] * len(engs)
+
+        def run(k):
+            for _ in range(steps):
+                res[k] = engs[k].verify_jobs_packed(packs[k])
+
+        barrier()
+        t1 = time.perf_counter()
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(len(engs))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        barrier()
+        el = time.perf_counter() - t1
+        for r in res:
+            assert np.array_equal(np.asarray(r), wl.expected), "e2e verdicts differ"
+        return {"value_e2e": round(wl.packed.n_sets * steps * len(engs) / el, 1),
+                "e2e": {"engines": len(engs), "steps_per_engine": steps, "seconds": round(el, 3),
+                        "input_bytes_per_batch": int(sum(x.nbytes for x in (packs[0].job_off, packs[0].pk_off,
+                                                                               packs[0].msgs, packs[0].sigs,
+                                                                               packs[0].pk_indices))),
+                        "path": "lb_verify_jobs_indexed from pinned host buffers: chunking + H2D + kernels + D2H"}}
+    finally:
+        for p in keep:
+            lib.lb_host_free(p)
+
+
+def extra_legs(a, engs, barrier, W, wl_main=None):
     """Secondary measurements (rank 0 at N = 1; each bounded to a few seconds)."""
     out = {}
     eng = engs[0]
+    if wl_main is not None:
+        out.update(e2e_leg(a, engs, barrier, W, wl_main))
     # one invalid attestation per slot: the failing root's search, batches in flight
     wi = W.make(eng, "c3_invalid", slots=a.slots)
     batches = [e.upload(W.indexed_for(e, wi)) for e in engs]
@@ -251,7 +322,7 @@ def extra_legs(a, engs, barrier, W):
     out["latency_block_ms"] = median_ms(lambda: eng.verify_jobs_packed(ip2), 10)
     # the other BASELINE configs at one batch in flight (resident inputs)
     per = {}
-    for name in ("c1", "c2", "c4", "c5"):
+    for name in ("c1", "c2", "c4", "c5", "c5_64"):
         wl = W.make(eng, name)
         b = eng.upload(W.indexed_for(eng, wl))
         got = b.verify()
@@ -295,13 +366,28 @@ def dropin_leg(a, W, eng_factory):
             f.write(np.ascontiguousarray(arr).tobytes())
         path = f.name
     try:
-        r = subprocess.run([node, os.path.join(ROOT, "tools", "bench_dropin.js"), path, str(a.dropin_engines), "3"],
-                           capture_output=True, text=True, timeout=300)
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "bench_dropin.js"), path, str(a.dropin_engines),
+                            str(a.dropin_rounds)], capture_output=True, text=True, timeout=300)
     finally:
         os.unlink(path)
     if r.returncode != 0:
         return {"error": (r.stdout + r.stderr)[-500:]}
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def signing_roots_leg():
+    """getBlockSignatureSets + GPU merkleization from the TS host's side (lodestar_amd/js/signing_roots.js
+    through addon.merkleize): the K3 devnet block, a 128-attestation block and a 32-block segment,
+    against the reference's ~45 ms per 100-signature block (verifyBlocksSignatures.ts:41-43)."""
+    import shutil
+    node = shutil.which("node")
+    if node is None:
+        return {"error": "node not installed"}
+    r = subprocess.run([node, os.path.join(ROOT, "tests", "js", "test_signing_roots.js"), "gpu"],
+                       capture_output=True, text=True, timeout=240)
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-500:]}
+    return json.loads(r.stdout.strip().splitlines()[-2])
 
 
 def main():
@@ -422,7 +508,7 @@ def main():
     solo = rank == 0 and world == 1 and not a.no_extra and a.workload == "c3" and not a.exchange
     extra, dropin, wc1 = {}, None, None
     if solo:
-        extra, wc1 = extra_legs(a, engs, barrier, W)
+        extra, wc1 = extra_legs(a, engs, barrier, W, wl)
     for e in engs:
         e.close()
     if solo:
@@ -430,6 +516,10 @@ def main():
             dropin = dropin_leg(a, W, lambda: Engine(local))
         except Exception as e:  # reported, never fatal
             dropin = {"error": repr(e)}
+        try:
+            extra["signing_roots"] = signing_roots_leg()
+        except Exception as e:  # reported, never fatal
+            extra["signing_roots"] = {"error": repr(e)}
     cpu = cpu_c1 = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:

@@ -119,7 +119,8 @@ struct lb_engine {
   dbuf y_root;  // FE value of the root check (the search starts from it)
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   // batches with at most this many distinct roots run their Miller loops one wave per root
-  // (k_miller_wave); larger ones one lane per root (k_miller_grouped).  LB_MILLER_WAVE_MAX.
+  // (k_miller_wave); larger ones 8 lanes per root, 32 roots per workgroup (k_miller_g8).
+  // LB_MILLER_WAVE_MAX.
   uint32_t miller_wave_max = 2048;
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
@@ -756,8 +757,9 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                            e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
       else
-        hipLaunchKernelGGL(k_miller_grouped, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
-                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+        hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,
+                           e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
+                           e->treeP.as<uint32_t>());
     }
     {
       stage_scope sc(e, ST_TREE_P, s1);

@@ -9,7 +9,7 @@
 //   k_hash_finish      per root  : Q0 + Q1, clear cofactor, to affine        (hash_to_G2, second half)
 //   k_pk_chunks[_idx] / k_pk_blind per set: G1 aggregation (utils.ts:5-16), r*PK
 //   k_gsum_*           per root  : P_u = sum r_i PK_i over the root's live sets
-//   k_miller_grouped   per root  : ML(P_u, H(m_u))                         (Pairing.mul_n_aggregate)
+//   k_miller_g8 / _wave per root : ML(P_u, H(m_u))                        (Pairing.mul_n_aggregate)
 //   k_msm_*            per set   : S = sum r_i sig_i (bucket MSM)
 //   k_tree_up_U / k_ml_S / k_root_check : product tree, ML(-G1, S), one final exponentiation
 //   k_rmsm_*, k_range_pk, k_search_check : the invalid-set search after a failing root
@@ -29,7 +29,9 @@
                        // but half the register file lets another batch's kernels co-reside
 #endif
 #ifndef LB_MINW_SUB
-#define LB_MINW_SUB LB_MINW_DEC  // k_sig_subgroup
+#define LB_MINW_SUB 1  // k_sig_subgroup: one wave per SIMD lets the compiler spill to AGPRs (8 B of
+                       // scratch instead of 696 B per lane; round 2 ran 2 waves and moved 564 MB
+                       // of spill traffic per 116k-set launch)
 #endif
 #ifndef LB_SUBGROUP_INL
 #define LB_SUBGROUP_INL true  // k_sig_subgroup: Fp products inline (no call-boundary spills)
@@ -81,6 +83,7 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 #include "lb_wave.h"
+#include "lb_group_exec.h"
 #include "lb_group.h"
 #include "lb_ssz.h"
 
@@ -453,31 +456,16 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 }
 
 // ---------------------------------------------------------------- Miller loops
-// Grouped loops: ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u
-// (bilinearity: prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into
-// leaf m + u of the message product tree (stride 2m).  Lanes u >= *n_u are idle.
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller_grouped(uint32_t n, uint32_t m,
-                                                           const uint32_t* __restrict__ n_u,
-                                                           const uint32_t* __restrict__ gp_aff,
-                                                           const uint32_t* __restrict__ gp_inf,
-                                                           const uint32_t* __restrict__ h_aff,
-                                                           uint32_t* __restrict__ treeP) {
-  uint32_t u = lb_tid();
-  if (u >= *n_u) return;
-  fp12 f = fp12_one();
-  if (!gp_inf[u]) {
-    g1a p = soa_ld<g1a>(gp_aff, n, u);
-    g2a h = soa_ld<g2a>(h_aff, n, u);
-    f = miller_loop_inl(p, h);
-  }
-  soa_st(treeP, 2 * m, m + u, f);
-}
-
+// ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u (bilinearity:
+// prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into leaf m + u of the
+// message product tree (stride 2m).  Two forms: k_miller_g8 (lb_group_exec.h: 8 lanes per root,
+// 32 roots per workgroup, the state in LDS -- large batches) and k_miller_wave below (one wave
+// per root -- batches with few distinct roots).
 // The same loops one wave per root (w_miller: the doubling / addition steps as wave programs,
 // their ~100 Fp products spread over the lanes).  A lone lane runs a Miller loop's 6 664 serial
 // Fp products in ~12 ms whatever the batch, so for a batch with few distinct roots (one slot of
-// gossip, one block, a single set) this cuts the per-root chain; k_miller_grouped stays the
-// throughput form for large batches (64 roots per wave).  Lanes 0-5 stage P_u (2 Fp) and H(m_u)
+// gossip, one block, a single set) this cuts the per-root chain; k_miller_g8 is the throughput
+// form for large batches.  Lanes 0-5 stage P_u (2 Fp) and H(m_u)
 // (4 Fp) from the SoA arrays.
 __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
                                                     const uint32_t* __restrict__ gp_aff,

@@ -18,8 +18,10 @@
  *
  * Exports:
  *   createEngine(device: number) -> External
- *       (the first call raises GPU_MAX_HW_QUEUES to 16 unless the environment set it, so the
- *       two HIP streams of each engine get their own hardware queue)
+ *       (the first call raises GPU_MAX_HW_QUEUES to 16 when it is unset or lower -- HIP's and the
+ *       GPU boxes' default is 4 -- so the three HIP streams of each engine get their own hardware
+ *       queue)
+ *   hwQueues() -> number    (the GPU_MAX_HW_QUEUES the HIP runtime was initialised with)
  *   destroyEngine(engine)   (deferred until the engine's in-flight requests have settled)
  *   verifyJobs(engine, jobOffsets: Uint32Array, setPkOffsets: Uint32Array,
  *              pubkeys: Uint8Array (96 B per key) | pkIndices: Uint32Array (resident table),
@@ -131,11 +133,11 @@ static napi_value create_engine(napi_env env, napi_callback_info info) {
   if (argc >= 1) NAPI_CALL(env, napi_get_value_int32(env, argv[0], &device));
   if (!queues_set) {
     /* HIP reads GPU_MAX_HW_QUEUES once, at runtime initialisation (the first engine): each
-     * engine drives two streams, and with the default 4 queues the streams of concurrent
-     * engines would share hardware queues (false dependencies).  A value set by the operator
-     * wins; the cap of 32 is the pool's limit. */
+     * engine drives three streams, and with the default 4 queues the streams of concurrent
+     * engines would share hardware queues (false dependencies between independent batches).
+     * A value of 16 or more set by the operator wins; the cap of 32 is the pool's limit. */
     const char* v = getenv("GPU_MAX_HW_QUEUES");
-    if (!v || !*v) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    if (!v || !*v || atoi(v) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
     queues_set = 1;
   }
   engine_box* b = (engine_box*)calloc(1, sizeof(engine_box));
@@ -524,6 +526,51 @@ static napi_value g1_decompress(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+/* merkleize(engine, chunkOffsets: Uint32Array (nTrees + 1), chunks: Uint8Array (32 B each),
+ *            depths: Uint32Array (nTrees), mixLengths: BigUint64Array (nTrees; 2^64 - 1 = no mix))
+ *   -> Uint8Array (32-byte roots): lb_merkleize, the SSZ hashing of signing-root production
+ *   (getBlockSignatureSets -> computeSigningRoot, state-transition/src/util/signingRoot.ts:7-13);
+ *   synchronous, one launch per call (js/signing_roots.js batches every tree of one level). */
+static napi_value merkleize(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  engine_box* b = NULL;
+  tview off, ch, dep, mix;
+  if (argc < 5 || napi_get_value_external(env, argv[0], (void**)&b) != napi_ok || !b || !b->e ||
+      !get_view(env, argv[1], &off) || !off.present || off.type != napi_uint32_array || off.n < 1 ||
+      !get_view(env, argv[2], &ch) || !ch.present || ch.type != napi_uint8_array || ch.n % 32 ||
+      !get_view(env, argv[3], &dep) || !dep.present || dep.type != napi_uint32_array || dep.n != off.n - 1 ||
+      !get_view(env, argv[4], &mix) || !mix.present || mix.type != napi_biguint64_array || mix.n != off.n - 1) {
+    napi_throw_type_error(env, NULL,
+                          "merkleize(engine, chunkOffsets: Uint32Array, chunks: Uint8Array, depths: Uint32Array, "
+                          "mixLengths: BigUint64Array)");
+    return NULL;
+  }
+  const uint32_t n = (uint32_t)dep.n;
+  const uint32_t* o = (const uint32_t*)off.data;
+  if (o[0] != 0 || (size_t)o[n] * 32 != ch.n) {
+    napi_throw_type_error(env, NULL, "merkleize: chunk offsets do not match the chunk bytes");
+    return NULL;
+  }
+  for (uint32_t t = 0; t < n; t++)
+    if (o[t + 1] < o[t] || ((const uint32_t*)dep.data)[t] > 63 ||
+        (uint64_t)(o[t + 1] - o[t]) > (1ull << ((const uint32_t*)dep.data)[t])) {
+      napi_throw_type_error(env, NULL, "merkleize: a tree has more chunks than 2^depth");
+      return NULL;
+    }
+  napi_value ab, out;
+  void* po;
+  NAPI_CALL(env, napi_create_arraybuffer(env, (size_t)(n ? n : 1) * 32, &po, &ab));
+  if (n) {
+    const int32_t st = lb_merkleize(b->e, n, o, (const uint8_t*)ch.data, (const uint32_t*)dep.data,
+                                    (const uint64_t*)mix.data, (uint8_t*)po);
+    if (st != LB_OK) return throw_code(env, st);
+  }
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, (size_t)n * 32, ab, 0, &out));
+  return out;
+}
+
 /* KZG group work (util/kzg.ts ckzg calls; synchronous, like c-kzg's) */
 static napi_value kzg_load_setup(napi_env env, napi_callback_info info) {
   size_t argc = 3;
@@ -606,6 +653,14 @@ static napi_value table_size(napi_env env, napi_callback_info info) {
   return v;
 }
 
+static napi_value hw_queues(napi_env env, napi_callback_info info) {
+  (void)info;
+  const char* v = getenv("GPU_MAX_HW_QUEUES");
+  napi_value r;
+  NAPI_CALL(env, napi_create_int32(env, v && *v ? atoi(v) : 4, &r));
+  return r;
+}
+
 static napi_value error_name(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], s;
@@ -628,6 +683,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"g1Decompress", NULL, g1_decompress, NULL, NULL, NULL, napi_default, NULL},
       {"aggregateSignatures", NULL, aggregate_signatures, NULL, NULL, NULL, napi_default, NULL},
       {"errorName", NULL, error_name, NULL, NULL, NULL, napi_default, NULL},
+      {"hwQueues", NULL, hw_queues, NULL, NULL, NULL, napi_default, NULL},
+      {"merkleize", NULL, merkleize, NULL, NULL, NULL, napi_default, NULL},
       {"kzgLoadSetup", NULL, kzg_load_setup, NULL, NULL, NULL, napi_default, NULL},
       {"g1Lincomb", NULL, g1_lincomb, NULL, NULL, NULL, napi_default, NULL},
       {"kzgVerifyProof", NULL, kzg_verify_proof, NULL, NULL, NULL, napi_default, NULL},

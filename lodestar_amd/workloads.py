@@ -24,7 +24,7 @@ Shapes (jobs = verifySignatureSets calls after chunkifyMaximizeChunkSize(sets, 1
       invalid sets at >= 1/1000 split between well-formed wrong-message signatures (-> false)
       and malformed bytes (32-byte signature -> BLST_INVALID_SIZE, cleared compression flag
       -> BLST_BAD_ENCODING), SURVEY.md §8(d) (configs[3])
-  c5  range sync: 32 blocks of c2 shape, one call per block (configs[4])
+  c5  range sync: 32 blocks of c2 shape, one call per block (configs[4]); c5_64: 64 blocks
 """
 from __future__ import annotations
 
@@ -234,8 +234,15 @@ def c5_specs(rng, n_blocks: int = 32):
     return [_block(rng, 11 + b) for b in range(n_blocks)]
 
 
+def c5_64_specs(rng):
+    """range sync at the reference's own sizing: a 64-block batch (~8 000 sets per 64 blocks,
+    multithread/index.ts:34)"""
+    return c5_specs(rng, n_blocks=64)
+
+
 SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c3_distinct": c3_distinct_specs,
-         "c3_invalid": c3_invalid_specs, "c3_mixed": c3_mixed_specs, "c4": c4_specs, "c5": c5_specs}
+         "c3_invalid": c3_invalid_specs, "c3_mixed": c3_mixed_specs, "c4": c4_specs, "c5": c5_specs,
+         "c5_64": c5_64_specs}
 
 
 def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:

@@ -408,7 +408,7 @@ def test_all_valid_distinct_roots_pass_at_the_root(engine):
     assert prof["search_msm"] == 0.0
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c4", "c5", "c5_64"])
 def test_baseline_config_workloads(engine, name):
     """BASELINE.json configs as verification batches (lodestar_amd/workloads.py): per-job verdicts
     equal the planted expectation (c4 carries invalid sets -> fallback + bisection), through both
@@ -577,8 +577,9 @@ def test_direct_verify_callers(engine):
 @pytest.mark.parametrize("name", ["c3_mixed", "c2"])
 def test_per_root_kernel_forms_agree(monkeypatch, name):
     """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
-    lane per root (k_hash_finish, k_miller_grouped) and many lanes per root (k_hash_finish_g8:
-    8-lane G2 doublings / additions; k_miller_wave: the wave engine); likewise the signatures'
+    lane per root (k_hash_finish) or 8 lanes per root (k_miller_g8, grouped LDS programs) and many
+    lanes per root (k_hash_finish_g8: 8-lane G2 doublings / additions; k_miller_wave: the wave
+    engine); likewise the signatures'
     subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count), S = sum r_i sig_i (bucket
     MSM / per-set terms, one lane or 8 lanes per set, + trees, by set count) and the invalid-set
     search's weighted range sums (bucket MSM / per-position 8-lane terms + segmented sums).

@@ -85,3 +85,55 @@ def test_js_kzg_gpu_matches_python(engine):
     blobs = [blob(0), blob(7)]
     assert got["commitments"] == [k.blob_to_kzg_commitment(b).hex() for b in blobs]
     assert got["proof"] == k.compute_aggregate_kzg_proof(blobs).hex()
+
+
+SR_SCRIPT = os.path.join(ROOT, "tests", "js", "test_signing_roots.js")
+
+
+def _ops_file(tmp_path):
+    import json
+    from conftest import load_json
+    from test_signing_roots import _operations_block
+    p = tmp_path / "ops_block.json"
+    p.write_text(json.dumps(_operations_block(load_json("k3_devnet.json"))))
+    return str(p)
+
+
+def _python_ops_roots(ops_path):
+    import json
+    from conftest import load_json
+    from lodestar_amd import signing_roots as SR
+    from test_signing_roots import cpu_merkleize, k3_state
+    blk = json.loads(open(ops_path).read())
+    sets = SR.resolve(SR.block_signature_sets(blk, k3_state(load_json("k3_devnet.json"))), cpu_merkleize)
+    return [{"name": s.name, "root": s.signing_root.hex(), "keys": [bytes(k).hex() for k in s.pubkeys]} for s in sets]
+
+
+def test_js_signing_roots_cpu(tmp_path):
+    """lodestar_amd/js/signing_roots.js (getBlockSignatureSets for the TS host): the K3 devnet roots,
+    and an operations block (slashing, exit, BLS change) equal to the Python walk's"""
+    if NODE is None:
+        pytest.skip("node not installed")
+    import json
+    ops = _ops_file(tmp_path)
+    r = subprocess.run([NODE, SR_SCRIPT, "cpu", ops], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[-1] == "js signing roots cpu ok"
+    assert json.loads(lines[-2]) == _python_ops_roots(ops)
+
+
+@pytest.mark.gpu
+def test_js_signing_roots_gpu(tmp_path):
+    """the same walk through addon.merkleize (lb_merkleize), plus its timings"""
+    if NODE is None:
+        pytest.skip("node not installed")
+    import json
+    ops = _ops_file(tmp_path)
+    r = subprocess.run([NODE, SR_SCRIPT, "gpu", ops], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[-1] == "js signing roots gpu ok"
+    out = json.loads(lines[-2])
+    assert out["ops"] == _python_ops_roots(ops)
+    print("signing-root timings:", {k: v for k, v in out.items() if k != "ops"})

@@ -63,3 +63,14 @@ def test_c3_invalid_and_mixed_shapes():
     flat = [s for j in mixed for s in j]
     assert sum(s.invalid for s in flat) >= 4
     assert sum(s.malformed == "short32" for s in flat) >= 4 and sum(s.malformed == "flag" for s in flat) >= 4
+
+
+def test_c5_block_counts():
+    """range sync: 32 blocks (BASELINE configs[4]) and the reference's own 64-block sizing
+    (multithread/index.ts:34: ~8 000 sets per 64 blocks), one non-batchable call per block"""
+    rng = np.random.default_rng(1)
+    for name, nb in (("c5", 32), ("c5_64", 64)):
+        jobs = W.SPECS[name](rng)
+        assert len(jobs) == nb
+        n = sum(len(j) for j in jobs)
+        assert 125 * nb <= n <= 135 * nb  # ~131 sets per C2-shaped block

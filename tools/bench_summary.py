@@ -7,8 +7,8 @@ r = d["roofline"] or {}
 print("value", d["value"], "single", d["value_one_batch_in_flight"], "distinct", d.get("value_distinct_roots"),
       "ms/step", d["ms_per_step"])
 print(" ".join(f"{k}={v['ms']}" for k, v in r.get("stages", {}).items()))
-for k in ("value_one_invalid_per_batch", "value_slots1", "latency_slot1_ms", "latency_1set_ms", "latency_block_ms",
-          "value_dropin", "batch_latency_ms"):
+for k in ("value_one_invalid_per_batch", "value_e2e", "value_slots1", "latency_slot1_ms", "latency_1set_ms",
+          "latency_block_ms", "value_dropin", "batch_latency_ms", "dropin", "signing_roots"):
     if k in d:
         print(k, d[k])
 for k in ("slots1_stage_ms", "latency_1set_stage_ms"):

@@ -21,7 +21,7 @@ def active_waves(k, grid):
         return w
     n = grid if k != "k_hash_map" else grid // 2
     mu = 1 << max(n - 1, 1).bit_length()
-    if k in ("k_hash_finish", "k_miller_grouped", "k_gsum_final"):
+    if k in ("k_hash_finish", "k_miller_g8", "k_gsum_final"):
         return -(-NU // 64)
     if k == "k_hash_map":
         return -(-2 * NU // 64)

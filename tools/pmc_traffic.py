@@ -24,7 +24,7 @@ STAGES = {
     "pk_blind": ["k_pk_blind"],
     "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
     "group_sum": ["k_gsum_chunks", "k_gsum_final"],
-    "miller": ["k_miller_grouped"],
+    "miller": ["k_miller_g8"],
     "tree_up_P": ["k_tree_up_U"],
     "ml_S": ["k_ml_S"],
     "root_check": ["k_root_check"],
