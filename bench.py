@@ -9,7 +9,8 @@ One process per GPU.  Under torchrun (WORLD_SIZE set) every rank runs main(); `-
 N > 1 and no WORLD_SIZE relaunches itself under torch.distributed.run (127.0.0.1) before any GPU
 call.  Each rank verifies its own shard (weak scaling: sets shard across GPUs with no data-path
 collective; --exchange adds the 576-byte Fp12 partial all-gather over RCCL and one final
-exponentiation per step).  A batch = B slots of gossip drained into one device
+exponentiation per step, SURVEY.md §8(e), with the same batches in flight: one process group per
+in-flight slot).  A batch = B slots of gossip drained into one device
 batch (default 6); F batches are in flight per GPU (default 7 = the engine cap per device,
 independent engines; 5 / 6 / 7 in flight measured 9.7 / 10.4 / 10.9 M sets/s in one A/B call).  A step =
 lb_batch_verify over one resident batch: all kernels + CSPRNG scalars + per-job result readback.
@@ -76,6 +77,8 @@ def parse():
                     help="skip the secondary measurement with every signing root distinct (c3_distinct)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (invalid-set, slots1, latencies, per-config, drop-in)")
+    ap.add_argument("--legs", default="e2e,invalid,slots1,latency,configs,dropin,roots",
+                    help="secondary legs to run (comma list; A/B runs pick one)")
     ap.add_argument("--dropin-engines", type=int, default=4)
     ap.add_argument("--dropin-rounds", type=int, default=10, help="drop-in leg: timed rounds (median reported)")
     return ap.parse_args()
@@ -166,17 +169,19 @@ def roofline(counts, packed, stage_ms):
             "device_ms": round(wall, 3), "stages": per}
 
 
-def run_inflight(batches, steps, expected, barrier):
+def run_inflight(batches, steps, expected, barrier, step_fns=None):
     """len(batches) batches in flight: independent engines (own streams + workspaces), one host
-    thread each, every engine verifying its own resident copy of the slot `steps` times."""
+    thread each, every engine verifying its own resident copy of the slot `steps` times
+    (step_fns[k]() instead of batches[k].verify() when given: the --exchange steps)."""
     import threading
-    for b in batches[1:]:
-        b.verify()
+    fns = step_fns or [b.verify for b in batches]
+    for f in fns[1:]:
+        f()
     res = [None] * len(batches)
 
     def run(k):
         for _ in range(steps):
-            res[k] = batches[k].verify()
+            res[k] = fns[k]()
 
     barrier()
     t1 = time.perf_counter()
@@ -274,9 +279,25 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     """Secondary measurements (rank 0 at N = 1; each bounded to a few seconds)."""
     out = {}
     eng = engs[0]
-    if wl_main is not None:
+    legs = set(a.legs.split(","))
+    if wl_main is not None and "e2e" in legs:
         out.update(e2e_leg(a, engs, barrier, W, wl_main))
-    # one invalid attestation per slot: the failing root's search, batches in flight
+    if "invalid" in legs:
+        out.update(invalid_leg(a, engs, barrier, W))
+    wc1 = W.make(eng, "c1")
+    if "slots1" in legs:
+        out.update(slots1_leg(a, eng, W))
+    if "latency" in legs:
+        out.update(latency_leg(eng, W, wc1))
+    if "configs" in legs:
+        out["per_config"] = configs_leg(a, eng, W)
+    return out, wc1
+
+
+def invalid_leg(a, engs, barrier, W):
+    """one invalid attestation per slot: the failing root's search, batches in flight"""
+    out = {}
+    eng = engs[0]
     wi = W.make(eng, "c3_invalid", slots=a.slots)
     batches = [e.upload(W.indexed_for(e, wi)) for e in engs]
     codes = batches[0].verify()
@@ -299,7 +320,12 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     out["invalid_batch_stage_ms"] = {k: round(v, 3) for k, v in prof.items() if v > 0}
     for b in batches:
         b.free()
-    # one slot per batch, one batch in flight
+    return out
+
+
+def slots1_leg(a, eng, W):
+    """one slot per batch, one batch in flight"""
+    out = {}
     w1 = W.make(eng, "c3")
     b1 = eng.upload(W.indexed_for(eng, w1))
     b1.verify()
@@ -308,8 +334,12 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     out["latency_slot1_ms"] = lat
     out["slots1_stage_ms"] = profiled_stages(eng, b1.verify)
     b1.free()
-    # small calls through the workspace path (lb_verify_jobs_indexed: upload + verify + readback)
-    wc1 = W.make(eng, "c1")
+    return out
+
+
+def latency_leg(eng, W, wc1):
+    """small calls through the workspace path (lb_verify_jobs_indexed: upload + verify + readback)"""
+    out = {}
     ip = W.indexed_for(eng, wc1)
     one = W.PackedJobs(job_off=np.array([0, 1], np.uint32), pk_off=np.array([0, 1], np.uint32), pubkeys=None,
                        msgs=ip.msgs[:32], sigs=ip.sigs[:96], sig_sizes=None, pk_indices=ip.pk_indices[:1])
@@ -320,7 +350,11 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     ip2 = W.indexed_for(eng, wc2)
     assert eng.verify_jobs_packed(ip2) == list(wc2.expected)
     out["latency_block_ms"] = median_ms(lambda: eng.verify_jobs_packed(ip2), 10)
-    # the other BASELINE configs at one batch in flight (resident inputs)
+    return out
+
+
+def configs_leg(a, eng, W):
+    """the other BASELINE configs at one batch in flight (resident inputs)"""
     per = {}
     for name in ("c1", "c2", "c4", "c5", "c5_64"):
         wl = W.make(eng, name)
@@ -342,8 +376,7 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
                 per[name]["cpu_threads"] = c["cores"]
             except Exception as e:  # reported, never fatal
                 per[name]["cpu_error"] = repr(e)
-    out["per_config"] = per
-    return out, wc1
+    return per
 
 
 def dropin_leg(a, W, eng_factory):
@@ -440,15 +473,26 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def step():
-        if a.exchange and world > 1:
+    # --exchange: every batch in flight has its own process group (created in the same order on
+    # every rank), so the engines' all-gathers of different batches proceed independently
+    groups = [None] * a.inflight
+    if a.exchange and world > 1:
+        groups = [dist.new_group(list(range(world))) for _ in range(a.inflight)]
+
+    def make_step(k):
+        b, e = batches[k], engs[k]
+        if not (a.exchange and world > 1):
+            return b.verify
+        from lodestar_amd.distributed import verify_sharded
+
+        def xstep():
             # 576-byte partials over RCCL, one final exponentiation of their product (distributed.py)
-            from lodestar_amd.distributed import verify_sharded
-            codes, _ = verify_sharded(batch.partial, eng.product_is_one, batch.verify,
+            codes, _ = verify_sharded(b.partial, e.product_is_one, b.verify, group=groups[k],
                                       device=coll_dev if coll_dev.type == "cuda" else None)
-        else:
-            codes = batch.verify()
-        return codes
+            return codes
+        return xstep
+
+    step = make_step(0)
 
     for _ in range(a.warmup):
         codes = step()
@@ -468,9 +512,9 @@ def main():
     eng.set_profiling(False)
     stage_ms = {k: v / a.steps for k, v in stage_ms.items()}
     el = el_single
-    inflight = a.inflight if not a.exchange else 1
+    inflight = a.inflight
     if inflight > 1:
-        el = run_inflight(batches, a.steps, wl.expected, barrier)
+        el = run_inflight(batches, a.steps, wl.expected, barrier, [make_step(k) for k in range(inflight)])
     el_t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -511,11 +555,12 @@ def main():
         extra, wc1 = extra_legs(a, engs, barrier, W, wl)
     for e in engs:
         e.close()
-    if solo:
+    if solo and "dropin" in a.legs.split(","):
         try:
             dropin = dropin_leg(a, W, lambda: Engine(local))
         except Exception as e:  # reported, never fatal
             dropin = {"error": repr(e)}
+    if solo and "roots" in a.legs.split(","):
         try:
             extra["signing_roots"] = signing_roots_leg()
         except Exception as e:  # reported, never fatal

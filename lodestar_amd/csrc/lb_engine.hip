@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -119,9 +120,11 @@ struct lb_engine {
   dbuf y_root;  // FE value of the root check (the search starts from it)
   uint64_t msg_key = 0;  // keyed probe hash (CSPRNG)
   // batches with at most this many distinct roots run their Miller loops one wave per root
-  // (k_miller_wave); larger ones 8 lanes per root, 32 roots per workgroup (k_miller_g8).
-  // LB_MILLER_WAVE_MAX.
+  // (k_miller_wave); larger ones one lane per root (k_miller_lane) while other batches are in
+  // flight on the device, else 8 lanes per root (k_miller_g8).  LB_MILLER_WAVE_MAX;
+  // LB_MILLER_FORM = lane | g8 pins the large-batch form (default: by device load).
   uint32_t miller_wave_max = 2048;
+  int miller_form = 0;  // 0 by load, 1 lane, 2 g8
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
@@ -165,6 +168,14 @@ struct lb_engine {
 // asynchronously instead of returning an error).  LB_MAX_ENGINES_PER_DEVICE overrides the cap.
 static std::mutex g_engine_mu;
 static int g_engine_count[64];
+// Batches currently inside the pipeline per device (all engines of the process).  With more than
+// one, the device is throughput-bound and the per-root kernels take their work-efficient forms.
+static std::atomic<int> g_device_busy[64];
+struct busy_scope {
+  int dev;
+  explicit busy_scope(int d) : dev(d) { g_device_busy[dev].fetch_add(1, std::memory_order_relaxed); }
+  ~busy_scope() { g_device_busy[dev].fetch_sub(1, std::memory_order_relaxed); }
+};
 static int max_engines_per_device() {
   const char* v = getenv("LB_MAX_ENGINES_PER_DEVICE");
   int k = v ? atoi(v) : 0;
@@ -263,6 +274,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
+  if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
@@ -293,6 +305,23 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   for (int i = 0; i < kStages; i++) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
+  }
+  // Size s1's scratch now, one engine at a time, for the one-lane per-root kernels with large
+  // private segments (k_miller_lane, k_hash_finish): an empty dispatch over more waves than the
+  // device holds.  Several queues growing their scratch at the same moment (batches in flight
+  // switching to the one-lane form together) abort with HSA_STATUS_ERROR_OUT_OF_RESOURCES.
+  {
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    if (e->n_u.ensure(4) != hipSuccess || hipMemsetAsync(e->n_u.p, 0, 4, e->stream) != hipSuccess) {
+      lb_engine_destroy(e);
+      return LB_ERR_DEVICE;
+    }
+    hipLaunchKernelGGL(k_miller_lane, dim3(4096), dim3(LB_TPB), 0, e->stream, 0u, 1u, e->n_u.as<uint32_t>(), nullptr,
+                       nullptr, nullptr, nullptr);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) {
+      lb_engine_destroy(e);
+      return LB_ERR_DEVICE;
+    }
   }
   *out = e;
   return LB_OK;
@@ -753,8 +782,13 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_MILLER, s1);
+      const bool shared = e->miller_form == 1 ||
+                          (e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1);
       if (nuh <= e->miller_wave_max)
         hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+      else if (shared)
+        hipLaunchKernelGGL(k_miller_lane, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                            e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
       else
         hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,
@@ -1297,6 +1331,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
   uint32_t m = 1, mu = 1;
+  busy_scope busy(e->device);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   // root verdict on s1 (after the join)
@@ -1343,6 +1378,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
     fp12_to_be576(out576, fp12_one());
     return LB_OK;
   }
+  busy_scope busy(e->device);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));

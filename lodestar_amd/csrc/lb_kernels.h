@@ -9,7 +9,7 @@
 //   k_hash_finish      per root  : Q0 + Q1, clear cofactor, to affine        (hash_to_G2, second half)
 //   k_pk_chunks[_idx] / k_pk_blind per set: G1 aggregation (utils.ts:5-16), r*PK
 //   k_gsum_*           per root  : P_u = sum r_i PK_i over the root's live sets
-//   k_miller_g8 / _wave per root : ML(P_u, H(m_u))                        (Pairing.mul_n_aggregate)
+//   k_miller_lane / _g8 / _wave per root : ML(P_u, H(m_u))               (Pairing.mul_n_aggregate)
 //   k_msm_*            per set   : S = sum r_i sig_i (bucket MSM)
 //   k_tree_up_U / k_ml_S / k_root_check : product tree, ML(-G1, S), one final exponentiation
 //   k_rmsm_*, k_range_pk, k_search_check : the invalid-set search after a failing root
@@ -29,9 +29,11 @@
                        // but half the register file lets another batch's kernels co-reside
 #endif
 #ifndef LB_MINW_SUB
-#define LB_MINW_SUB 1  // k_sig_subgroup: one wave per SIMD lets the compiler spill to AGPRs (8 B of
-                       // scratch instead of 696 B per lane; round 2 ran 2 waves and moved 564 MB
-                       // of spill traffic per 116k-set launch)
+#define LB_MINW_SUB LB_MINW_DEC  // k_sig_subgroup.  One wave per SIMD lets the compiler spill to
+                       // AGPRs instead of scratch (8 B instead of 696 B per lane) but costs occupancy:
+                       // 10.2 vs 10.6 M sets/s at 7 in flight, 4.9 vs 5.0 M at one (round-3 A/B,
+                       // profiles/r3_variants_ab.txt); the ladder state in LDS instead (24 KB per
+                       // wave) still spilled and ran 4.7 M at one in flight.
 #endif
 #ifndef LB_SUBGROUP_INL
 #define LB_SUBGROUP_INL true  // k_sig_subgroup: Fp products inline (no call-boundary spills)
@@ -458,15 +460,31 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 // ---------------------------------------------------------------- Miller loops
 // ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u (bilinearity:
 // prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into leaf m + u of the
-// message product tree (stride 2m).  Two forms: k_miller_g8 (lb_group_exec.h: 8 lanes per root,
-// 32 roots per workgroup, the state in LDS -- large batches) and k_miller_wave below (one wave
-// per root -- batches with few distinct roots).
-// The same loops one wave per root (w_miller: the doubling / addition steps as wave programs,
-// their ~100 Fp products spread over the lanes).  A lone lane runs a Miller loop's 6 664 serial
-// Fp products in ~12 ms whatever the batch, so for a batch with few distinct roots (one slot of
-// gossip, one block, a single set) this cuts the per-root chain; k_miller_g8 is the throughput
-// form for large batches.  Lanes 0-5 stage P_u (2 Fp) and H(m_u)
-// (4 Fp) from the SoA arrays.
+// message product tree (stride 2m).  Three forms, picked per launch (lb_engine.hip):
+//   * k_miller_lane: one lane per root, 64 roots per wave.  The fewest instructions per root
+//     (the tower formulas compiled straight, operand sums computed once), but ~12 ms of serial
+//     products per lane and a large private segment; the form when the device is shared with
+//     other batches in flight, whose waves fill the SIMDs while these wait.
+//   * k_miller_g8 (lb_group_exec.h): 8 lanes per root, 32 roots per workgroup, the state in LDS:
+//     ~3x shorter, ~2.5x more VALU work per root; the form for a large batch alone on the device.
+//   * k_miller_wave below: one wave per root, for batches with few distinct roots.
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller_lane(uint32_t n, uint32_t m,
+                                                                const uint32_t* __restrict__ n_u,
+                                                                const uint32_t* __restrict__ gp_aff,
+                                                                const uint32_t* __restrict__ gp_inf,
+                                                                const uint32_t* __restrict__ h_aff,
+                                                                uint32_t* __restrict__ treeP) {
+  const uint32_t u = lb_tid();
+  if (u >= *n_u) return;
+  fp12 f = fp12_one();
+  if (!gp_inf[u]) {
+    const g1a p = soa_ld<g1a>(gp_aff, n, u);
+    const g2a h = soa_ld<g2a>(h_aff, n, u);
+    f = miller_loop_inl(p, h);
+  }
+  soa_st(treeP, 2 * m, m + u, f);
+}
+
 __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
                                                     const uint32_t* __restrict__ gp_aff,
                                                     const uint32_t* __restrict__ gp_inf,

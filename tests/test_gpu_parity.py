@@ -531,6 +531,27 @@ def test_search_c3_invalid_two_slots(engine):
     assert (wl.expected == 0).sum() == 2
 
 
+@pytest.mark.parametrize("knob", ["LB_SEARCH_MERGE=0", "LB_SEARCH_ROOTSUM=0", "LB_SEARCH_PRE=1"])
+def test_search_forms_find_the_same_sets(monkeypatch, knob):
+    """Every selectable form of the invalid-set search (lb_engine.hip: look-ahead tests in a
+    separate launch pair, round 1 over the bucket MSM instead of per-root sums, later rounds over
+    the kept per-set terms) names exactly the planted jobs of c3 with one wrong attestation per
+    slot (2 slots: above LB_SEARCH_SMALL_MAX, so the root-level rounds run)."""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    k, v = knob.split("=")
+    monkeypatch.setenv(k, v)
+    with Engine(0) as e:
+        wl = W.make(e, "c3_invalid", slots=2)
+        b = e.upload(W.indexed_for(e, wl))
+        try:
+            got = np.asarray(b.verify())
+        finally:
+            b.free()
+    assert np.array_equal(got, wl.expected), (knob, np.nonzero(got != wl.expected))
+    assert (wl.expected == 0).sum() == 2
+
+
 def test_aggregate_signatures_golden(engine):
     """bls.Signature.aggregate on the GPU against the oracle's golden
     groups: sums (with duplicates, cancellation to infinity, infinity members), the first bad
@@ -577,7 +598,7 @@ def test_direct_verify_callers(engine):
 @pytest.mark.parametrize("name", ["c3_mixed", "c2"])
 def test_per_root_kernel_forms_agree(monkeypatch, name):
     """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
-    lane per root (k_hash_finish) or 8 lanes per root (k_miller_g8, grouped LDS programs) and many
+    lane per root (k_hash_finish, k_miller_lane) or 8 lanes per root (k_miller_g8, grouped LDS programs) and many
     lanes per root (k_hash_finish_g8: 8-lane G2 doublings / additions; k_miller_wave: the wave
     engine); likewise the signatures'
     subgroup check (k_sig_subgroup / k_sig_subgroup_g8, by set count), S = sum r_i sig_i (bucket
@@ -590,8 +611,10 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     from lodestar_amd import workloads as W
     outs = []
     big = str(1 << 31)
-    # (all one-lane / MSM forms), (many-lane forms, one-lane S terms), (many-lane forms, 8-lane S terms)
-    for lim, s_g8 in (("0", "0"), (big, "0"), (big, big)):
+    # (all one-lane / MSM forms), (the same with 8-lane Miller loops), (many-lane forms, one-lane
+    # S terms), (many-lane forms, 8-lane S terms)
+    for lim, s_g8, mform in (("0", "0", "lane"), ("0", "0", "g8"), (big, "0", "g8"), (big, big, "lane")):
+        monkeypatch.setenv("LB_MILLER_FORM", mform)
         monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
         monkeypatch.setenv("LB_SUBGROUP_G8_MAX", lim)
@@ -609,4 +632,4 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
                 b.free()
         assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
         outs.append(part)
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]

@@ -6,7 +6,7 @@ for r in $LB_RUNS; do
   unset LODESTAR_BLS_LIB
   envs=""
   case "$r" in
-    env:*) envs="${r#env:}" ;;
+    env:*) envs="${r#env:}"; envs=${envs//+/ } ;;
     lib:*) export LODESTAR_BLS_LIB=$GRAFT_REPO_ROOT/build/variants/${r#lib:}.so ;;
   esac
   tag=$(echo "$r" | tr ':=/' '___')
