@@ -143,6 +143,10 @@ struct lb_engine {
   dbuf s_root, rs_idx, s_set;
   bool search_rootsum = true;
   bool search_pre = false;  // later rounds take [w] of the kept per-set terms (LB_SEARCH_PRE)
+  // large batches: the first round checks the root tree's top subtrees directly, their S_j from
+  // one 4-window bucket MSM over all sets, without look-ahead tests and without the per-root sums
+  // (one GLV ladder per set); LB_SEARCH_BLOCKS=0 restores the per-root sums + look-ahead round
+  bool search_blk = true;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -283,6 +287,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_MERGE")) e->search_merge = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -979,8 +984,11 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
     mlo.swap(rlo);
     mpre.swap(rpre);
   }
-  const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * LB_SMSM_NB;
-  const uint32_t bcap = (2 * LB_SMSM_W * T) / LB_GROUP_CHUNK + nb;
+  // weight-1 instances only: 32-bit GLV halves, 4 windows instead of 6
+  const bool w4 = std::all_of(mmode.begin(), mmode.end(), [](uint32_t m) { return m == 0u; });
+  const uint32_t nwin = w4 ? (uint32_t)LB_MSM_W : (uint32_t)LB_SMSM_W;
+  const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * nwin * LB_MSM_B;
+  const uint32_t bcap = (2 * nwin * T) / LB_GROUP_CHUNK + nb;
   LB_HIP(sx_up(e, SX_KIND, dk, s1));
   LB_HIP(sx_up(e, SX_KEY, dkey, s1));
   LB_HIP(sx_up(e, SX_LO, dlo, s1));
@@ -1052,33 +1060,48 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       LB_HIP(e->bch.ensure((size_t)(nb + 1) * 4));
       LB_HIP(e->bchunk_beg.ensure((size_t)bcap * 4));
       LB_HIP(e->bchunk_end.ensure((size_t)bcap * 4));
-      LB_HIP(e->bmembers.ensure((size_t)2 * LB_SMSM_W * (T ? T : 1) * 4));
+      LB_HIP(e->bmembers.ensure((size_t)2 * nwin * (T ? T : 1) * 4));
       LB_HIP(e->bacc.ensure((size_t)bcap * sizeof(g2j)));
       LB_HIP(e->bsum.ensure((size_t)nb * sizeof(g2j)));
       LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)nb * 4, s1));
       LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)nb * 4, s1));
       const smsm_args ma{U(SX_MPRE), U(SX_MLO), U(SX_MMODE), U(SX_MWA), U(SX_MWB)};
       if (T) {
-        hipLaunchKernelGGL(k_smsm_count, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
-                           e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
-                           e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+        if (w4)
+          hipLaunchKernelGGL(k_smsm_count<LB_MSM_W>, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma,
+                             e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                             e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
+        else
+          hipLaunchKernelGGL(k_smsm_count<LB_SMSM_W>, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma,
+                             e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                             e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
       }
       hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
                          e->bchunk_end.as<uint32_t>());
       if (T) {
-        hipLaunchKernelGGL(k_smsm_scatter, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
-                           e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),
-                           e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(), e->bcursor.as<uint32_t>(),
-                           e->bmembers.as<uint32_t>());
+        if (w4)
+          hipLaunchKernelGGL(k_smsm_scatter<LB_MSM_W>, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma,
+                             e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                             e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
+                             e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
+        else
+          hipLaunchKernelGGL(k_smsm_scatter<LB_SMSM_W>, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma,
+                             e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                             e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
+                             e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
       }
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
       hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
-      hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(64 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
-                         U(SX_S), cm, 0u);
+      if (w4)
+        hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(cm), dim3(64 * LB_MSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
+                           U(SX_S), cm, 0u);
+      else
+        hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(64 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
+                           U(SX_S), cm, 0u);
     }
     if (c)
       hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),
@@ -1190,7 +1213,9 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
   LB_HIP(hipMemcpyAsync(x.members.data(), e->members.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipMemcpyAsync(root.y.data(), e->y_root.p, 576, hipMemcpyDeviceToHost, e->stream));
   LB_HIP(hipStreamSynchronize(e->stream));
-  if (e->search_rootsum && x.nu > 1 && n > e->search_small_max) {
+  // the first round's form for large batches (see lb_engine::search_blk)
+  const bool r1_plain = e->search_blk && x.nu > 1 && n > e->search_small_max;
+  if (!r1_plain && e->search_rootsum && x.nu > 1 && n > e->search_small_max) {
     const int32_t st = search_root_sums(e, x);
     if (st != LB_OK) return st;
     x.rs = true;
@@ -1255,7 +1280,7 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
           inst += c.kind != 2u;
           test_job t{c, {}, false, di};
           search_children(x, c, false, t.ch);
-          if (t.ch.size() >= 2) {
+          if (t.ch.size() >= 2 && !(r1_plain && round == 1)) {
             ahead.push_back(std::move(t));
             inst++;
           }

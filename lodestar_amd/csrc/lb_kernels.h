@@ -856,7 +856,8 @@ __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* 
 // subtrees of 2^b roots from root a) weight ((set_uid_i - a) >> b) + 1, mode 2 (a weighted test
 // over parts of a members) weight (position offset / a) + 1.  Weights are <= LB_WT_MAX, so
 // both 32-bit GLV halves of r_i w stay below 2^(32 + LB_WT_BITS) <= 2^48: LB_SMSM_W = 6 windows
-// of 8 bits, instance j owning buckets [j LB_SMSM_NB, (j+1) LB_SMSM_NB).
+// of 8 bits, instance j owning buckets [j LB_SMSM_NB, (j+1) LB_SMSM_NB).  A round of weight-1
+// instances only (the first round's direct checks) takes LB_MSM_W = 4 windows (32-bit halves).
 #define LB_WT_MAX 1024  // children of a weighted test over parts of one root (lb_engine.hip kWtParts)
 #define LB_WT_BITS 11
 #define LB_SMSM_W 6
@@ -884,6 +885,7 @@ __device__ __forceinline__ bool smsm_member(const smsm_args& a, uint32_t c, uint
   wt = md == 0u ? 1u : (md == 1u ? ((set_uid[i] - a.wa[j]) >> a.wb[j]) + 1u : off / a.wa[j] + 1u);
   return true;
 }
+template <int W>
 __global__ void __launch_bounds__(LB_TPB) k_smsm_count(uint32_t T, uint32_t c, smsm_args a,
                                                        const uint32_t* __restrict__ members,
                                                        const uint32_t* __restrict__ set_uid,
@@ -899,12 +901,13 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_count(uint32_t T, uint32_t c, s
   const uint64_t wd = scalars[i];
   LB_UNROLL for (int h = 0; h < 2; h++) {
     const uint64_t k = (uint64_t)(uint32_t)(wd >> (32 * h)) * wt;
-    LB_UNROLL for (int w = 0; w < LB_SMSM_W; w++) {
+    LB_UNROLL for (int w = 0; w < W; w++) {
       const uint32_t d = (uint32_t)(k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
-      if (d) atomicAdd(&cnt[j * LB_SMSM_NB + w * LB_MSM_B + d], 1u);
+      if (d) atomicAdd(&cnt[j * (W * LB_MSM_B) + w * LB_MSM_B + d], 1u);
     }
   }
 }
+template <int W>
 __global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c, smsm_args a,
                                                          const uint32_t* __restrict__ members,
                                                          const uint32_t* __restrict__ set_uid,
@@ -921,10 +924,10 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c,
   const uint64_t wd = scalars[i];
   LB_UNROLL for (int h = 0; h < 2; h++) {
     const uint64_t k = (uint64_t)(uint32_t)(wd >> (32 * h)) * wt;
-    LB_UNROLL for (int w = 0; w < LB_SMSM_W; w++) {
+    LB_UNROLL for (int w = 0; w < W; w++) {
       const uint32_t d = (uint32_t)(k >> (LB_MSM_C * w)) & (LB_MSM_B - 1);
       if (d) {
-        const uint32_t b = j * LB_SMSM_NB + w * LB_MSM_B + d;
+        const uint32_t b = j * (W * LB_MSM_B) + w * LB_MSM_B + d;
         bmembers[boff[b] + atomicAdd(&cursor[b], 1u)] = i | ((uint32_t)h << 31);
       }
     }
