@@ -64,6 +64,28 @@ __device__ __forceinline__ void soa_st(uint32_t* __restrict__ base, uint32_t n, 
   for (int i = 0; i < (int)(sizeof(T) / 4); i++) base[(size_t)i * n + e] = w[i];
 }
 
+// Array-of-structures element e (16-byte vector accesses): for arrays read by gathers (a lane
+// pulls its element's 144 or 192 contiguous bytes instead of one word from each of 36 or 48
+// SoA rows, i.e. 36 or 48 separate cache lines).
+template <class T>
+__device__ __forceinline__ T aos_ld(const uint32_t* __restrict__ base, uint32_t e) {
+  static_assert(sizeof(T) % 16 == 0, "16-byte multiples");
+  T r;
+  uint4* w = reinterpret_cast<uint4*>(&r);
+  const uint4* s = reinterpret_cast<const uint4*>(base) + (size_t)e * (sizeof(T) / 16);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) w[i] = s[i];
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void aos_st(uint32_t* __restrict__ base, uint32_t e, const T& v) {
+  static_assert(sizeof(T) % 16 == 0, "16-byte multiples");
+  const uint4* w = reinterpret_cast<const uint4*>(&v);
+  uint4* d = reinterpret_cast<uint4*>(base) + (size_t)e * (sizeof(T) / 16);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = w[i];
+}
+
 template <int N>
 __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict__ src) {
   static_assert(N % 16 == 0, "16-byte multiples");
@@ -452,7 +474,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
     rj = jac_infinity<fp>();
   }
   if (!act) return;
-  soa_st(rpk, n, i, rj);
+  aos_st(rpk, i, rj);  // AoS: the per-root sums and the search gather it by member
   if (ok) soa_st(pk_aff, n, i, pk);  // the unblinded aggregate, for single-set checks of the search
   pk_status[i] = st;
 }
@@ -1046,7 +1068,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, c
   g1j acc = jac_infinity<fp>();
   for (uint32_t k = rlo[j]; k < rlo[j] + rlen[j]; k++) {
     const uint32_t i = members[k];
-    if (set_live[i]) acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));
+    if (set_live[i]) acc = jac_add_i<fp, true>(acc, aos_ld<g1j>(rpk, i));
   }
   soa_st(pk_out, c, j, acc);
 }
@@ -1073,7 +1095,7 @@ __global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __r
       const uint32_t a = lo + k * pp, e = lo + (k * pp + pp < len ? k * pp + pp : len);
       for (uint32_t x = a; x < e; x++) {
         const uint32_t i = members[x];
-        if (set_live[i]) run = jac_add_i<fp, true>(run, soa_ld<g1j>(rpk, n, i));
+        if (set_live[i]) run = jac_add_i<fp, true>(run, aos_ld<g1j>(rpk, i));
       }
       if (q >= 1) s1 = jac_add_i<fp, true>(s1, run);
     }
@@ -1375,7 +1397,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t i = members[k];
     if (!set_live[i]) continue;
-    acc = jac_add_i<fp, true>(acc, soa_ld<g1j>(rpk, n, i));  // r*PK Jacobian (infinity handled)
+    acc = jac_add_i<fp, true>(acc, aos_ld<g1j>(rpk, i));  // r*PK Jacobian (infinity handled)
   }
   soa_st(gacc, n, c, acc);
 }

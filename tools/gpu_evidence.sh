@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out/full/ev
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 ONE="--steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --no-distinct --no-extra"
-R=${R:-r2}
+R=${R:-r3}
 echo "== pmc: FETCH_SIZE"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/full/ev/pmc_fetch -o $R --output-format csv -- python3 bench.py $ONE > gpurun_out/full/ev/pmc_fetch.log 2>&1 || { tail -3 gpurun_out/full/ev/pmc_fetch.log; exit 1; }
 echo "== pmc: WRITE_SIZE"

@@ -16,15 +16,15 @@ import sys
 
 # bench.py stage -> the kernels its stage_scope brackets (lb_engine.hip run_pipeline)
 STAGES = {
-    "decode_sigs": ["k_decompress_sigs", "k_sig_subgroup", "k_job_status"],
+    "decode_sigs": ["k_decompress_sigs", "k_sig_subgroup", "k_sig_subgroup_g8", "k_job_status"],
     "dedup": ["k_msg_insert", "k_msg_count", "k_msg_scatter"],
     "hash_map": ["k_hash_map"],
-    "hash_finish": ["k_hash_finish"],
+    "hash_finish": ["k_hash_finish", "k_hash_finish_g8"],
     "pk_chunks": ["k_pk_chunks", "k_pk_chunks_idx"],
     "pk_blind": ["k_pk_blind"],
     "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
     "group_sum": ["k_gsum_chunks", "k_gsum_final"],
-    "miller": ["k_miller_g8"],
+    "miller": ["k_miller_g8", "k_miller_lane", "k_miller_wave"],
     "tree_up_P": ["k_tree_up_U"],
     "ml_S": ["k_ml_S"],
     "root_check": ["k_root_check"],
