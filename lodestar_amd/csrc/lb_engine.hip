@@ -147,6 +147,9 @@ struct lb_engine {
   // one 4-window bucket MSM over all sets, without look-ahead tests and without the per-root sums
   // (one GLV ladder per set); LB_SEARCH_BLOCKS=0 restores the per-root sums + look-ahead round
   bool search_blk = true;
+  // distinct roots numbered in hash-table order (pseudo-random) rather than input order, so the
+  // search's first-round subtrees hold comparable numbers of sets (LB_ROOT_SHUFFLE=0: input order)
+  bool root_shuffle = true;
   std::vector<uint64_t> h_scalars;
   // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
   dbuf table, table_flag;
@@ -288,6 +291,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   const char* pv = getenv("LB_S1_PRIORITY");
   const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
@@ -697,8 +701,13 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       LB_HIP(hipMemsetAsync(e->n_u.p, 0, 4, s1));
       LB_HIP(hipMemsetAsync(e->gcnt.p, 0, (size_t)n * 4, s1));
       hipLaunchKernelGGL(k_msg_insert, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(), e->msg_key,
-                         cap, e->msg_tab.as<uint32_t>(), e->rep_of.as<uint32_t>(), e->uid_of.as<uint32_t>(),
-                         e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
+                         cap, e->msg_tab.as<uint32_t>(), e->rep_of.as<uint32_t>());
+      if (e->root_shuffle)
+        hipLaunchKernelGGL(k_msg_uid, dim3(nblk(cap)), dim3(LB_TPB), 0, s1, cap, e->msg_tab.as<uint32_t>(),
+                           e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_msg_uid_input, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
+                           e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
                          e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
                          e->gpos.as<uint32_t>());

@@ -320,18 +320,44 @@ LB_HD fp lb_tab8(const fp* t, uint32_t k) {
     default: return t[7];
   }
 }
+// Inline products for the exponentiation chains (fenced so the compiler keeps one product's
+// columns live at a time): a lone lane's out-of-line product costs ~1.42 us of latency against
+// ~1.05 us inline, and ~7 % more issue (tools/ubench/fpmul_ps.hip, profiles/r3_variants_ab.txt).
+LB_HD fp fp_mul_inl(const fp& a, const fp& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+  const fp r = fp_mul28(a, b);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+#else
+  return fp_mul(a, b);
+#endif
+}
+LB_HD fp fp_sqr_inl(const fp& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+  const fp r = fp_sqr28(a);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+#else
+  return fp_sqr(a);
+#endif
+}
+template <bool kInlMul = false>
 LB_HD fp fp_pow_const_i(fp a, const uint32_t* e, int top_bit) {
+  auto mul = [](const fp& x, const fp& y) { return kInlMul ? fp_mul_inl(x, y) : fp_mul(x, y); };
+  auto sqr = [](const fp& x) { return kInlMul ? fp_sqr_inl(x) : fp_sqr(x); };
   fp tab[8];
   tab[0] = a;
-  const fp a2 = fp_sqr(a);
-  LB_UNROLL for (int k = 1; k < 8; k++) tab[k] = fp_mul(tab[k - 1], a2);
+  const fp a2 = sqr(a);
+  LB_UNROLL for (int k = 1; k < 8; k++) tab[k] = mul(tab[k - 1], a2);
   auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
   fp r = fp_zero();
   bool first = true;
   int i = top_bit;
   while (i >= 0) {
     if (!bit(i)) {
-      r = fp_sqr(r);
+      r = sqr(r);
       i--;
       continue;
     }
@@ -343,8 +369,8 @@ LB_HD fp fp_pow_const_i(fp a, const uint32_t* e, int top_bit) {
       r = lb_tab8(tab, val >> 1);
       first = false;
     } else {
-      for (int k = i; k >= j; k--) r = fp_sqr(r);
-      r = fp_mul(r, lb_tab8(tab, val >> 1));
+      for (int k = i; k >= j; k--) r = sqr(r);
+      r = mul(r, lb_tab8(tab, val >> 1));
     }
     i = j - 1;
   }
@@ -447,7 +473,10 @@ LB_NI fp fp_inv_plain_vt(fp a) { return fp_inv_plain_vt_i(a); }
 // Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
 LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
 LB_HD fp fp_inv_i(const fp& a) { return fp_mul(fp_inv_plain_vt_i(a), fp_load(LB_R3)); }
-LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) { return fp_pow_const_i(a, e, top_bit); }
+#ifndef LB_POW_INL
+#define LB_POW_INL true  // exponentiations with inline products (A/B: false = out-of-line fp_mul_v)
+#endif
+LB_NI fp fp_pow_const(fp a, const uint32_t* e, int top_bit) { return fp_pow_const_i<LB_POW_INL>(a, e, top_bit); }
 LB_HD fp fp_sqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_SQRT, 378); }   // a^((p+1)/4)
 LB_HD fp fp_isqrt_cand(const fp& a) { return fp_pow_const(a, LB_EXP_ISQRT, 378); }  // a^((p-3)/4)
 // Quadratic character by the binary Jacobi-symbol algorithm (variable time; every input is
@@ -579,7 +608,7 @@ template <bool kInl = false>
 LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp alpha;
-  if constexpr (kInl) alpha = fp_pow_const_i(norm, LB_EXP_SQRT, 378);
+  if constexpr (kInl) alpha = fp_pow_const_i<LB_POW_INL>(norm, LB_EXP_SQRT, 378);
   else alpha = fp_sqrt_cand(norm);  // sqrt(norm) if it exists
   fp inv2 = fp_load(LB_INV2);
   fp d1 = fp_mul(fp_add(a.c0, alpha), inv2);
@@ -589,7 +618,7 @@ LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   // z = delta^((p-3)/4), s = delta z = delta^((p+1)/4), and s z = delta^((p-1)/2) = +-1, so
   // 1/s = +-z: the square root and the inverse it needs come from one exponentiation
   fp z;
-  if constexpr (kInl) z = fp_pow_const_i(delta, LB_EXP_ISQRT, 378);
+  if constexpr (kInl) z = fp_pow_const_i<LB_POW_INL>(delta, LB_EXP_ISQRT, 378);
   else z = fp_isqrt_cand(delta);
   fp s = fp_mul(delta, z);
   bool delta_qr = fp_eq(fp_sqr(s), delta);

@@ -563,8 +563,7 @@ __device__ __forceinline__ uint32_t msg_hash(const uint8_t* __restrict__ msgs, u
 }
 __global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t* __restrict__ msgs, uint64_t key,
                                                        uint32_t cap, uint32_t* __restrict__ tab,
-                                                       uint32_t* __restrict__ rep_of, uint32_t* __restrict__ uid_of,
-                                                       uint32_t* __restrict__ uniq_set, uint32_t* __restrict__ n_u) {
+                                                       uint32_t* __restrict__ rep_of) {
   const uint32_t i = lb_tid();
   if (i >= n) return;
   uint32_t h = msg_hash(msgs, i, key) & (cap - 1u), rep = i;
@@ -578,11 +577,32 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t
     h = (h + 1u) & (cap - 1u);
   }
   rep_of[i] = rep;
-  if (rep == i) {
-    const uint32_t u = atomicAdd(n_u, 1u);
-    uid_of[i] = u;
-    uniq_set[u] = i;
-  }
+}
+// Unique-message ids in input order (the first set of each root, LB_ROOT_SHUFFLE=0)
+__global__ void __launch_bounds__(LB_TPB) k_msg_uid_input(uint32_t n, const uint32_t* __restrict__ rep_of,
+                                                          uint32_t* __restrict__ uid_of,
+                                                          uint32_t* __restrict__ uniq_set, uint32_t* __restrict__ n_u) {
+  const uint32_t i = lb_tid();
+  if (i >= n || rep_of[i] != i) return;
+  const uint32_t u = atomicAdd(n_u, 1u);
+  uid_of[i] = u;
+  uniq_set[u] = i;
+}
+// Unique-message ids in TABLE-SLOT order (keyed hash: pseudo-random, not the input order): the
+// roots' order is the root product tree's leaf order, and the invalid-set search's first-round
+// subtrees are runs of it.  In input order a run of 64 roots held whole committees of one slot
+// (16 k sets) and the failing subtrees' tests went through the 6-window bucket MSM; shuffled,
+// a subtree holds ~3.5 committee roots on average.
+__global__ void __launch_bounds__(LB_TPB) k_msg_uid(uint32_t cap, const uint32_t* __restrict__ tab,
+                                                    uint32_t* __restrict__ uid_of, uint32_t* __restrict__ uniq_set,
+                                                    uint32_t* __restrict__ n_u) {
+  const uint32_t h = lb_tid();
+  if (h >= cap) return;
+  const uint32_t i = tab[h];
+  if (i == 0xffffffffu) return;  // each distinct root holds exactly one slot (its first claimer's)
+  const uint32_t u = atomicAdd(n_u, 1u);
+  uid_of[i] = u;
+  uniq_set[u] = i;
 }
 
 // set_uid[i] = unique-message id of set i; pos[i] = its rank inside the group (cnt zeroed)

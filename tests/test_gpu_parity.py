@@ -531,13 +531,14 @@ def test_search_c3_invalid_two_slots(engine):
     assert (wl.expected == 0).sum() == 2
 
 
-@pytest.mark.parametrize("knobs", ["LB_SEARCH_MERGE=0", "LB_SEARCH_BLOCKS=0", "LB_SEARCH_BLOCKS=0+LB_SEARCH_MERGE=0",
+@pytest.mark.parametrize("knobs", ["LB_SEARCH_MERGE=0", "LB_ROOT_SHUFFLE=0", "LB_SEARCH_BLOCKS=0",
+                                   "LB_SEARCH_BLOCKS=0+LB_SEARCH_MERGE=0",
                                    "LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0", "LB_SEARCH_BLOCKS=0+LB_SEARCH_PRE=1"])
 def test_search_forms_find_the_same_sets(monkeypatch, knobs):
     """Every selectable form of the invalid-set search (lb_engine.hip: look-ahead tests in a
     separate launch pair; the first round over per-root sums with look-ahead tests instead of
     direct subtree checks from one 4-window MSM; that round over the 6-window bucket MSM; later
-    rounds over the kept per-set terms) names exactly the planted jobs of c3 with one wrong
+    rounds over the kept per-set terms; roots numbered in input order) names exactly the planted jobs of c3 with one wrong
     attestation per slot (2 slots: above LB_SEARCH_SMALL_MAX, so the large-batch rounds run)."""
     from lodestar_amd.engine import Engine
     from lodestar_amd import workloads as W
