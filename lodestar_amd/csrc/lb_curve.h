@@ -21,6 +21,16 @@ typedef jac<fp2> g2j;
 typedef aff<fp> g1a;
 typedef aff<fp2> g2a;
 
+// the same point over another field type of the same representation (fp <-> fpi)
+template <class T, class S>
+LB_HD aff<T> aff_as(const aff<S>& a) {
+  return aff<T>{T{a.x}, T{a.y}};
+}
+template <class T, class S>
+LB_HD jac<T> jac_as(const jac<S>& a) {
+  return jac<T>{T{a.x}, T{a.y}, T{a.z}};
+}
+
 template <class F>
 LB_HD jac<F> jac_infinity() {
   jac<F> r;

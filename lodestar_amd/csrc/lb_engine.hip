@@ -657,6 +657,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // ---- pubkeys, r*PK: on s3 beside the signature decode for batches up to small_s_max sets
     // (shortens the signature side's chain); on s2 before the decode for large batches, where the
     // two would contend with the per-root chain on s1 for the whole chip
+    // (also for a large batch alone on the device: its s1 chain then slowed by more than the s2
+    // chain gained, 5.2 -> 5.1 M sets/s, round-3 A/B)
     const hipStream_t s3 = n <= e->small_s_max ? s3_ : s2;
     {
       stage_scope sc(e, ST_PK_CHUNKS, s3);

@@ -796,7 +796,49 @@ LB_HD fp f_select(bool c, const fp& a, const fp& b) { return fp_select(c, a, b);
 LB_HD void f_set_zero(fp& a) { a = fp_zero(); }
 LB_HD void f_set_one(fp& a) { a = fp_one(); }
 
+// fp with inline (fenced) products: a kernel that instantiates the generic curve code on jac<fpi>
+// runs its G1 formulas without out-of-line product calls (k_pk_blind's GLV ladder)
+struct fpi : fp {};
+LB_HD fpi fpi_of(const fp& a) { return fpi{a}; }
+LB_HD fpi f_add(const fpi& a, const fpi& b) { return fpi{fp_add(a, b)}; }
+LB_HD fpi f_sub(const fpi& a, const fpi& b) { return fpi{fp_sub(a, b)}; }
+LB_HD fpi f_mul(const fpi& a, const fpi& b) { return fpi{fp_mul_inl(a, b)}; }
+LB_HD fpi f_sqr(const fpi& a) { return fpi{fp_sqr_inl(a)}; }
+LB_HD fpi f_dbl(const fpi& a) { return fpi{fp_dbl(a)}; }
+LB_HD fpi f_neg(const fpi& a) { return fpi{fp_neg(a)}; }
+LB_HD fpi f_mul3(const fpi& a) { return fpi{fp_mul3(a)}; }
+LB_HD fpi f_mul8(const fpi& a) { return fpi{fp_mul8(a)}; }
+LB_HD bool f_is_zero(const fpi& a) { return fp_is_zero(a); }
+LB_HD bool f_eq(const fpi& a, const fpi& b) { return fp_eq(a, b); }
+LB_HD fpi f_select(bool c, const fpi& a, const fpi& b) { return fpi{fp_select(c, a, b)}; }
+LB_HD void f_set_zero(fpi& a) { a = fpi{fp_zero()}; }
+LB_HD void f_set_one(fpi& a) { a = fpi{fp_one()}; }
+
 LB_HD fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
+// ... and fp2 with inline products (the G2 bucket sums and reductions of the MSM)
+struct fp2i : fp2 {};
+LB_HD fp2i f_add(const fp2i& a, const fp2i& b) { return fp2i{fp2_add(a, b)}; }
+LB_HD fp2i f_sub(const fp2i& a, const fp2i& b) { return fp2i{fp2_sub(a, b)}; }
+LB_HD fp2i f_mul(const fp2i& a, const fp2i& b) {
+  const fp t0 = fp_mul_inl(a.c0, b.c0);
+  const fp t1 = fp_mul_inl(a.c1, b.c1);
+  const fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return fp2i{fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)}};
+}
+LB_HD fp2i f_sqr(const fp2i& a) {
+  const fp t0 = fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  const fp t1 = fp_mul_inl(a.c0, a.c1);
+  return fp2i{fp2{t0, fp_dbl(t1)}};
+}
+LB_HD fp2i f_dbl(const fp2i& a) { return fp2i{fp2_dbl(a)}; }
+LB_HD fp2i f_neg(const fp2i& a) { return fp2i{fp2_neg(a)}; }
+LB_HD fp2i f_mul3(const fp2i& a) { return fp2i{fp2_mul3(a)}; }
+LB_HD fp2i f_mul8(const fp2i& a) { return fp2i{fp2_mul8(a)}; }
+LB_HD bool f_is_zero(const fp2i& a) { return fp2_is_zero(a); }
+LB_HD bool f_eq(const fp2i& a, const fp2i& b) { return fp2_eq(a, b); }
+LB_HD fp2i f_select(bool c, const fp2i& a, const fp2i& b) { return fp2i{fp2_select(c, a, b)}; }
+LB_HD void f_set_zero(fp2i& a) { a = fp2i{fp2_zero()}; }
+LB_HD void f_set_one(fp2i& a) { a = fp2i{fp2_one()}; }
 LB_HD fp2 f_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
 LB_HD fp2 f_mul(const fp2& a, const fp2& b) { return fp2_mul(a, b); }
 LB_HD fp2 f_sqr(const fp2& a) { return fp2_sqr(a); }

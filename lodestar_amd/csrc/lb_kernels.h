@@ -44,6 +44,18 @@
 #ifndef LB_MINW_GSUM
 #define LB_MINW_GSUM 1  // k_gsum_chunks (all-inline)
 #endif
+#ifndef LB_G1_INL
+#define LB_G1_INL 1  // k_pk_blind's GLV ladder with inline products (jac<fpi>); 0: out-of-line calls
+#endif
+#ifndef LB_G2_INL
+#define LB_G2_INL 1  // the MSM's G2 additions (chunks, buckets, reduction) with inline products
+#endif
+#if LB_G2_INL
+typedef fp2i lb_g2f;
+#else
+typedef fp2 lb_g2f;
+#endif
+typedef jac<lb_g2f> g2jm;
 #ifndef LB_MINW_G1
 #define LB_MINW_G1 2  // G1 kernels: one Fp multiply per step, so a second wave hides its latency
 #endif
@@ -469,7 +481,11 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
     // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
     const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
     const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
+#if LB_G1_INL
+    rj = jac_as<fp>(jac_mul_glv_i<fpi, true>(aff_as<fpi>(pk), aff_as<fpi>(t2), aff_as<fpi>(t3), scalars[i]));
+#else
     rj = jac_mul_glv_i<fp, true>(pk, t2, t3, scalars[i]);
+#endif
   } else {
     rj = jac_infinity<fp>();
   }
@@ -728,7 +744,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32
                                                        uint32_t* __restrict__ bacc, uint32_t nb) {
   const uint32_t c = lb_tid();
   if (c >= bch[nb]) return;
-  g2j acc = jac_infinity<fp2>();
+  g2jm acc = jac_infinity<lb_g2f>();
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t m = members[k], i = m & 0x7fffffffu;
     g2a p;
@@ -744,9 +760,9 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32
       p.x = fp2_mul_fp(p.x, fp_load(LB_PSI2_CX));
       p.y = fp2_neg(fp2_mul_fp(p.y, fp_load(LB_PSI2_CY)));
     }
-    acc = jac_add_aff_i<fp2, true>(acc, p);
+    acc = jac_add_aff_i<lb_g2f, true>(acc, aff_as<lb_g2f>(p));
   }
-  soa_st(bacc, cap, c, acc);
+  soa_st(bacc, cap, c, jac_as<fp2>(acc));
 }
 // bucket b = sum of its chunk sums (SoA, stride nb); empty buckets are infinity
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t* __restrict__ bch,
@@ -754,9 +770,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t*
                                                         uint32_t* __restrict__ bsum, uint32_t nb) {
   const uint32_t b = lb_tid();
   if (b >= nb) return;
-  g2j acc = jac_infinity<fp2>();
-  for (uint32_t c = bch[b]; c < bch[b + 1]; c++) acc = jac_add_i(acc, soa_ld<g2j>(bacc, cap, c));
-  soa_st(bsum, nb, b, acc);
+  g2jm acc = jac_infinity<lb_g2f>();
+  for (uint32_t c = bch[b]; c < bch[b + 1]; c++)
+    acc = jac_add_i<lb_g2f, true>(acc, jac_as<lb_g2f>(soa_ld<g2j>(bacc, cap, c)));
+  soa_st(bsum, nb, b, jac_as<fp2>(acc));
 }
 // One workgroup per MSM instance j of W windows (buckets [j W 256, (j+1) W 256) of bsum, stride
 // nb), one wave per window: lane s owns digits [4 s, 4 s + 4).  A lane's running sums give
@@ -781,33 +798,39 @@ __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restric
   const uint32_t s = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint32_t* bw = bsum;  // bucket (instance, w, d) at element blockIdx.x * W * 256 + w * 256 + d
   const uint32_t e0 = blockIdx.x * (W * LB_MSM_B) + w * LB_MSM_B + 4 * s;
-  g2j run = soa_ld<g2j>(bw, nb, e0 + 3);
-  g2j y = run;
-  run = jac_add_i(run, soa_ld<g2j>(bw, nb, e0 + 2));
-  y = jac_add_i(y, run);
-  run = jac_add_i(run, soa_ld<g2j>(bw, nb, e0 + 1));
-  y = jac_add_i(y, run);  // 3 B3 + 2 B2 + B1
-  g2j u = s ? jac_add_i(run, soa_ld<g2j>(bw, nb, e0)) : run;  // digit 0 is unused
+  // (out-of-line products here: inline ones grew this kernel's private segment 1.7 -> 4.3 KB)
+  typedef fp2 rf;
+  typedef jac<rf> g2jm;
+  auto ld = [&](uint32_t e) { return soa_ld<g2j>(bw, nb, e); };
+  auto add = [](const g2jm& a, const g2jm& b) { return jac_add_i(a, b); };
+  auto shfl = [](const g2jm& a, unsigned d) { return g2j_shfl_down(a, d); };
+  g2jm run = ld(e0 + 3);
+  g2jm y = run;
+  run = add(run, ld(e0 + 2));
+  y = add(y, run);
+  run = add(run, ld(e0 + 1));
+  y = add(y, run);  // 3 B3 + 2 B2 + B1
+  g2jm u = s ? add(run, ld(e0)) : run;  // digit 0 is unused
   // inclusive suffix scan: u_s = sum_{t >= s} T_t
   for (int l = 0; l < 6; l++) {  // rolled: the body is an inlined G2 addition
     const unsigned d = 1u << l;
-    const g2j o = g2j_shfl_down(u, d);
-    if (s + d < 64) u = jac_add_i(u, o);
+    const g2jm o = shfl(u, d);
+    if (s + d < 64) u = add(u, o);
   }
-  g2j v = y;
-  if (s) v = jac_add_i(v, jac_dbl_i(jac_dbl_i(u)));
+  g2jm v = y;
+  if (s) v = add(v, jac_dbl_i(jac_dbl_i(u)));
   for (int l = 5; l >= 0; l--) {
     const unsigned d = 1u << l;
-    const g2j o = g2j_shfl_down(v, d);
-    if (s < d) v = jac_add_i(v, o);
+    const g2jm o = shfl(v, d);
+    if (s < d) v = add(v, o);
   }
   if (s == 0) win[w] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    g2j S = win[W - 1];
+    g2jm S = win[W - 1];
     for (int ww = W - 2; ww >= 0; ww--) {
       for (int b = 0; b < LB_MSM_C; b++) S = jac_dbl_i(S);
-      S = jac_add_i(S, win[ww]);
+      S = add(S, win[ww]);
     }
     soa_st(out, n_out, out0 + blockIdx.x, S);
   }
