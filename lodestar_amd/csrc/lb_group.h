@@ -13,6 +13,8 @@
 #pragma once
 #include "lb_curve.h"
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;  // (as lb_wave.h)
+
 __device__ __forceinline__ int g8_q() { return threadIdx.x & 7; }
 __device__ __forceinline__ int g8_base() { return (threadIdx.x & 63) & ~7; }
 
@@ -226,4 +228,55 @@ __device__ __forceinline__ g2j g8_mul_2d(const g2j& t1, const g2j& t2, const g2j
 }
 __device__ __forceinline__ g2j g8_mul_glv(const g2j& t1, const g2j& t2, const g2j& t3, uint64_t w) {
   return g8_mul_2d(t1, t2, t3, w & 0xffffffffu, w >> 32, 32);
+}
+
+// The same with the long-lived points in LDS instead of registers: the replicated form holds p,
+// [x]p, psi(p) + [x]p and the partial sum (4 x 72 words per lane) across both ladders, which the
+// register file cannot hold beside a G2 addition's temporaries.  G: this group's 4 x 72 words of
+// LDS (every lane of the group writes and reads the same replicated values).
+__device__ __forceinline__ void g8_stash(lds_u32* G, int slot, const g2j& p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&p);
+  LB_UNROLL for (int k = 0; k < 72; k++) G[72 * slot + k] = w[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ g2j g8_unstash(const lds_u32* G, int slot) {
+  g2j p;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&p);
+  LB_UNROLL for (int k = 0; k < 72; k++) w[k] = G[72 * slot + k];
+  return p;
+}
+// [|x|] (point in slot s), the base re-read at the five additions
+__device__ __forceinline__ g2j g8_mul_xabs_st(const lds_u32* G, int s) {
+  g2j acc = g8_unstash(G, s);
+#pragma clang loop unroll(disable)
+  for (int i = 62; i >= 0; i--) {
+    g8_dbl(acc);
+    if ((LB_X_ABS >> i) & 1ull) g8_add(acc, g8_unstash(G, s));
+  }
+  return acc;
+}
+// h_eff p via psi (as g8_clear_cofactor); slots: 0 p, 1 t1 = [x]p, 2 t3, 3 t2 = psi(p) + t1
+__device__ __forceinline__ g2j g8_clear_cofactor_st(const g2j& p_in, lds_u32* G) {
+  g8_stash(G, 0, p_in);
+  g8_stash(G, 1, jac_neg(g8_mul_xabs_st(G, 0)));  // t1 = [x] p
+  {
+    g2j t3 = g8_unstash(G, 0);
+    g8_dbl(t3);
+    t3 = g8_psi2(t3);
+    g8_add(t3, jac_neg(g8_psi(g8_unstash(G, 0))));  // psi^2(2p) - psi(p)
+    g8_stash(G, 2, t3);
+  }
+  {
+    g2j t2 = g8_psi(g8_unstash(G, 0));
+    g8_add(t2, g8_unstash(G, 1));  // psi(p) + t1
+    g8_stash(G, 3, t2);
+  }
+  const g2j t2x = jac_neg(g8_mul_xabs_st(G, 3));  // [x](t1 + t2)
+  g2j t3 = g8_unstash(G, 2);
+  g8_add(t3, t2x);
+  g8_add(t3, jac_neg(g8_unstash(G, 1)));
+  g8_add(t3, jac_neg(g8_unstash(G, 0)));
+  return t3;
 }

@@ -50,6 +50,14 @@
 #ifndef LB_G2_INL
 #define LB_G2_INL 1  // the MSM's G2 additions (chunks, buckets, reduction) with inline products
 #endif
+#if LB_G1_INL
+typedef fpi lb_g1f;  // the G1 chunk and per-root sums' additions with inline products
+#else
+typedef fp lb_g1f;
+#endif
+#ifndef LB_G2_INL_SB
+#define LB_G2_INL_SB LB_G2_INL  // ... and k_sig_blind's per-set GLV ladder
+#endif
 #if LB_G2_INL
 typedef fp2i lb_g2f;
 #else
@@ -250,13 +258,15 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n
 __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                         const uint32_t* __restrict__ sig_inf,
                                                         int32_t* __restrict__ sig_status) {
+  __shared__ uint32_t g8s[8 * 72];  // the point, per group (re-read at the additions, not held)
   const uint32_t i = blockIdx.x * 8 + (threadIdx.x >> 3);
   if (i >= n) return;  // uniform within the group
   if (sig_status[i] != LB_OK || sig_inf[i]) return;
-  const g2j p = jac_from_aff(soa_ld<g2a>(sig_aff, n, i));
-  const g2j acc = g8_mul_xabs(p);
+  lds_u32* G = (lds_u32*)g8s + (threadIdx.x >> 3) * 72;
+  g8_stash(G, 0, jac_from_aff(soa_ld<g2a>(sig_aff, n, i)));
+  const g2j acc = g8_mul_xabs_st(G, 0);
   bool ok = !jac_is_inf(acc);  // psi(P) is finite
-  if (ok) ok = jac_eq(g8_psi(p), jac_neg(acc));
+  if (ok) ok = jac_eq(g8_psi(g8_unstash(G, 0)), jac_neg(acc));
   if (!ok && g8_q() == 0) sig_status[i] = LB_POINT_NOT_IN_GROUP;
 }
 
@@ -320,6 +330,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n,
 // Blocks of 64 threads = 8 roots; idle groups of the last block recompute the last root.
 __global__ void __launch_bounds__(64) k_hash_finish_g8(uint32_t n, const uint32_t* __restrict__ n_u,
                                                        const uint32_t* __restrict__ q, uint32_t* __restrict__ h_aff) {
+  __shared__ uint32_t g8s[8 * 4 * 72];  // g8_clear_cofactor_st's points, per group
   const uint32_t nu = *n_u;
   if (blockIdx.x * 8 >= nu) return;  // whole block idle (uniform: fp_inv_block is safe)
   const uint32_t u = blockIdx.x * 8 + (threadIdx.x >> 3);
@@ -327,7 +338,7 @@ __global__ void __launch_bounds__(64) k_hash_finish_g8(uint32_t n, const uint32_
   const uint32_t uc = act ? u : nu - 1;
   g2j h = soa_ld<g2j>(q, 2 * n, uc);
   g8_add(h, soa_ld<g2j>(q, 2 * n, n + uc));
-  h = g8_clear_cofactor(h);
+  h = g8_clear_cofactor_st(h, (lds_u32*)g8s + (threadIdx.x >> 3) * 4 * 72);
   const fp nz = fp_add(fp_sqr(h.z.c0), fp_sqr(h.z.c1));
   const bool zero = fp_is_zero(nz);
   const fp ni = fp_inv_block(zero ? fp_one() : nz);
@@ -382,7 +393,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
   if (c >= nc) return;
   uint32_t a = chunk_lo[c], e = chunk_lo[c + 1];
   int st = LB_OK;
-  g1j acc = jac_infinity<fp>();
+  jac<lb_g1f> acc = jac_infinity<lb_g1f>();
   for (uint32_t k = a; k < e; k++) {
     uint32_t t = idx[k];
     if (t >= table_n) {
@@ -395,9 +406,9 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
       break;
     }
     if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
-    acc = jac_add_aff_i<fp, true>(acc, soa_ld<g1a>(table, table_cap, t));
+    acc = jac_add_aff_i<lb_g1f, true>(acc, aff_as<lb_g1f>(soa_ld<g1a>(table, table_cap, t)));
   }
-  soa_st(chunk_acc, nc, c, acc);
+  soa_st(chunk_acc, nc, c, jac_as<fp>(acc));
   chunk_status[c] = st;
 }
 
@@ -887,7 +898,11 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_sig_blind(uint32_t n, c
     const fp2 zi{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
     const fp2 zi2 = fp2_sqr(zi);
     const g2a t3{fp2_mul(s.x, zi2), fp2_mul(fp2_mul(s.y, zi2), zi)};
+#if LB_G2_INL_SB
+    r = jac_as<fp2>(jac_mul_glv_i<fp2i, true>(aff_as<fp2i>(t1), aff_as<fp2i>(t2), aff_as<fp2i>(t3), scalars[i]));
+#else
     r = jac_mul_glv_i<fp2, true>(t1, t2, t3, scalars[i]);
+#endif
   }
   soa_st(terms, n, i, r);
 }
@@ -1436,13 +1451,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
                                                         uint32_t* __restrict__ gacc) {
   const uint32_t c = lb_tid();
   if (c >= gch[*n_u]) return;
-  g1j acc = jac_infinity<fp>();
+  jac<lb_g1f> acc = jac_infinity<lb_g1f>();
   for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
     const uint32_t i = members[k];
     if (!set_live[i]) continue;
-    acc = jac_add_i<fp, true>(acc, aos_ld<g1j>(rpk, i));  // r*PK Jacobian (infinity handled)
+    acc = jac_add_i<lb_g1f, true>(acc, jac_as<lb_g1f>(aos_ld<g1j>(rpk, i)));  // r*PK (infinity handled)
   }
-  soa_st(gacc, n, c, acc);
+  soa_st(gacc, n, c, jac_as<fp>(acc));
 }
 
 // P_u = sum of the group's chunk sums, to affine (one batched inversion per block); gp_inf[u]

@@ -10,4 +10,5 @@ for v in ${VARS:-}; do
 done
 runs=${LB_RUNS:-default}
 [ -z "${LB_RUNS:-}" ] && for v in ${VARS:-}; do runs="$runs lib:$v"; done
-LB_RUNS="$runs" AB_FLAGS="--steps 20 --warmup 5 ${LEGS:+--legs $LEGS} ${LEGS:---no-extra}" bash tools/gpu_ab_env.sh
+if [ -n "${LEGS:-}" ]; then legs="--legs $LEGS"; else legs="--no-extra"; fi
+LB_RUNS="$runs" AB_FLAGS="--steps 20 --warmup 5 $legs" bash tools/gpu_ab_env.sh
