@@ -319,7 +319,9 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   // private segments (k_miller_lane, k_hash_finish): an empty dispatch over more waves than the
   // device holds.  Several queues growing their scratch at the same moment (batches in flight
   // switching to the one-lane form together) abort with HSA_STATUS_ERROR_OUT_OF_RESOURCES.
-  {
+  // (Not when the one-lane Miller form is disabled, LB_MILLER_FORM=g8: the queue then never needs
+  // that private segment, and every queue's scratch counts against one per-process pool.)
+  if (e->miller_form != 2) {
     std::lock_guard<std::mutex> lk(g_engine_mu);
     if (e->n_u.ensure(4) != hipSuccess || hipMemsetAsync(e->n_u.p, 0, 4, e->stream) != hipSuccess) {
       lb_engine_destroy(e);
