@@ -896,6 +896,9 @@ static uint32_t parts_per(uint32_t len, bool direct) {
   const uint32_t f = direct ? 64u : kWtParts;
   return (len + f - 1) / f;
 }
+#ifndef LB_SEARCH_BISECT
+#define LB_SEARCH_BISECT 0  // 1: the round-2 form (halve such a node), for A/B builds
+#endif
 static void search_children(const search_ctx& x, const snode& a, bool direct, std::vector<snode>& out) {
   out.clear();
   if (a.kind == 2u || a.len <= 1) return;
@@ -910,7 +913,10 @@ static void search_children(const search_ctx& x, const snode& a, bool direct, st
   if (a.kind == 1u) return parts(a.key, a.lo, a.len);
   if (a.d == x.L) return parts(a.key - x.mu, a.lo, a.len);
   const int d = (int)a.d, L = (int)x.L;
-  int dd = direct ? std::max(d + 1, std::min(d + 7, L - 6)) : d + 6;
+  // direct children: subtrees of 64 roots (their weighted tests can name one failing root); a
+  // node of <= 64 roots whose weighted test matched nothing (>= 2 failing roots) is checked root by
+  // root in ONE round (halving it instead took up to six rounds for two wrong roots in a subtree)
+  int dd = direct ? (d >= L - 6 && !LB_SEARCH_BISECT ? L : std::max(d + 1, std::min(d + 7, L - 6))) : d + 6;
   if (dd > L) dd = L;
   const uint32_t k = (uint32_t)(dd - d), span = (uint32_t)(L - dd);
   for (uint32_t v = a.key << k; v < (a.key + 1) << k; v++) {
