@@ -177,6 +177,9 @@ static std::mutex g_engine_mu;
 static int g_engine_count[64];
 // Batches currently inside the pipeline per device (all engines of the process).  With more than
 // one, the device is throughput-bound and the per-root kernels take their work-efficient forms.
+#ifndef LB_HASH_ALONE_G8
+#define LB_HASH_ALONE_G8 1  // cofactor clearing by 8-lane groups whenever the device is otherwise idle (0: by root count only)
+#endif
 static std::atomic<int> g_device_busy[64];
 struct busy_scope {
   int dev;
@@ -686,6 +689,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
                          b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      // (8 lanes per signature also for a slot while the device is otherwise idle ran slower:
+      // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
       if (n <= e->subgroup_g8_max)
         hipLaunchKernelGGL(k_sig_subgroup_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
@@ -736,7 +741,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     }
     {
       stage_scope sc(e, ST_HASH_FIN, s1);
-      if (nuh <= e->hash_g8_max)
+      // 8 lanes per root when the device runs no other batch (a few hundred waves on 1 024 SIMDs:
+      // latency), one lane per root under load (2.5x less work), as for the Miller loops below
+      const bool alone = e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1;
+      if (nuh <= e->hash_g8_max || (LB_HASH_ALONE_G8 && alone))
         hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
                            e->h_aff.as<uint32_t>());
       else
