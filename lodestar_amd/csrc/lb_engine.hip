@@ -891,6 +891,8 @@ struct test_job {
   std::vector<snode> ch;
   bool fresh;    // y from the host (a node failing in an earlier round); else from direct check `d`
   uint32_t src;  // fresh: index into F; else index into D
+  int32_t spec = -1;    // a look-ahead test of child `spec_k` of fresh test `spec` (y: the parent's)
+  uint32_t spec_k = 0;
 };
 }  // namespace
 
@@ -904,6 +906,10 @@ static uint32_t parts_per(uint32_t len, bool direct) {
   const uint32_t f = direct ? 64u : kWtParts;
   return (len + f - 1) / f;
 }
+#ifndef LB_SEARCH_SPEC
+#define LB_SEARCH_SPEC 1  // look-ahead tests over the parts of a fresh test's roots, device idle (0: off; A/B builds)
+#endif
+static constexpr uint32_t kSpecMaxSets = 16384;  // ... for nodes of at most this many sets
 #ifndef LB_SEARCH_BISECT
 #define LB_SEARCH_BISECT 0  // 1: the round-2 form (halve such a node), for A/B builds
 #endif
@@ -1280,12 +1286,13 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
         break;
       }
     }
+    const bool spec_on = LB_SEARCH_SPEC && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1;
     for (size_t a = 0; a < work.size();) {
       // a launch set: whole failing nodes until the MSM instance budget is reached
       std::vector<fnode> Fs;
       std::vector<snode> D;
       std::vector<uint32_t> d_owner;  // D index -> Fs index
-      std::vector<test_job> fresh, ahead;
+      std::vector<test_job> fresh, spec, ahead;
       size_t inst = 0;
       while (a < work.size() && (Fs.empty() || inst < kMaxMsm)) {
         const fnode& f = work[a++];
@@ -1294,6 +1301,22 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
         if (!f.multi) {
           test_job t{f.s, {}, true, fi};
           search_children(x, f.s, false, t.ch);
+          // a weighted test over <= 64 ROOTS: in the same round, a weighted test over each root's
+          // parts, matched against the node's own y (if the node's test names root k, root k is the
+          // node's one failing child and y_k = y).  The named root's test then names the set, one
+          // round earlier; the other roots' tests are discarded.  Only while the device runs no
+          // other batch: under load their Miller loops and final exponentiations cost more than
+          // the round they save (profiles/r3_search_spec_ab.txt).
+          if (spec_on && !t.ch.empty() && t.ch[0].kind == 0u && t.ch[0].d == x.L && f.s.len <= kSpecMaxSets)
+            for (uint32_t k = 0; k < (uint32_t)t.ch.size(); k++) {
+              test_job g{t.ch[k], {}, true, fi};
+              search_children(x, t.ch[k], false, g.ch);
+              if (g.ch.size() < 2) continue;
+              g.spec = (int32_t)fresh.size();
+              g.spec_k = k;
+              spec.push_back(std::move(g));
+              inst++;
+            }
           fresh.push_back(std::move(t));
           inst++;
           continue;
@@ -1314,7 +1337,9 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
         }
       }
       std::vector<test_job> tests(fresh);
-      const uint32_t n_fresh = (uint32_t)fresh.size();
+      const uint32_t n_own = (uint32_t)fresh.size();
+      tests.insert(tests.end(), spec.begin(), spec.end());  // fresh too: y from the host
+      const uint32_t n_fresh = (uint32_t)tests.size();
       tests.insert(tests.end(), ahead.begin(), ahead.end());
       std::vector<int32_t> verdict, tout;
       std::vector<uint32_t> ydir;
@@ -1325,12 +1350,30 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
         std::fprintf(stderr, "[lb search] round %d: %zu failing nodes, %zu direct checks, %zu weighted tests: %.3f ms\n",
                      round, Fs.size(), D.size(), tests.size(),
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-      // fresh tests: the named child, or the node again with its children to check directly
-      for (uint32_t t = 0; t < n_fresh; t++) {
+      // fresh tests: the named child (or, by its look-ahead test, the named child's named part),
+      // or the node again with its children to check directly
+      std::vector<int32_t> spec_of;  // (own test, child) -> look-ahead test
+      std::vector<uint32_t> spec_base(n_own + 1, 0);
+      for (uint32_t t = n_own; t < n_fresh; t++) spec_base[tests[t].spec + 1]++;
+      for (uint32_t t = 0; t < n_own; t++) spec_base[t + 1] += spec_base[t];
+      for (uint32_t t = n_own; t < n_fresh; t++) spec_of.push_back((int32_t)t);  // grouped by own test, child order
+      for (uint32_t t = 0; t < n_own; t++) {
         const fnode& f = Fs[tests[t].src];
         const int k = tout[t];
-        if (k >= 1 && (size_t)k <= tests[t].ch.size()) next.push_back({tests[t].ch[k - 1], false, f.y});
-        else next.push_back({f.s, true, f.y});
+        if (k < 1 || (size_t)k > tests[t].ch.size()) {
+          next.push_back({f.s, true, f.y});
+          continue;
+        }
+        int32_t st = -1;
+        for (uint32_t q = spec_base[t]; q < spec_base[t + 1]; q++)
+          if (tests[spec_of[q]].spec_k == (uint32_t)(k - 1)) st = spec_of[q];
+        if (st < 0) {
+          next.push_back({tests[t].ch[k - 1], false, f.y});
+          continue;
+        }
+        const int k2 = tout[st];
+        if (k2 >= 1 && (size_t)k2 <= tests[st].ch.size()) next.push_back({tests[st].ch[k2 - 1], false, f.y});
+        else next.push_back({tests[t].ch[k - 1], true, f.y});
       }
       // direct checks: each failing child goes on by its weighted test
       std::vector<int> any_fail(Fs.size(), 0);

@@ -343,8 +343,140 @@ LB_HD fp fp_sqr_inl(const fp& a) {
   return fp_sqr(a);
 #endif
 }
+// Limb-resident exponentiation chains.  fp_mul28 / fp_sqr28 spend ~110 of their 632 / 506 VALU
+// instructions unpacking 12 x 32-bit operands into 28-bit limbs, repacking the result and
+// reducing it below p.  A chain of products can stay in limbs: with Montgomery radix R' = 2^392
+// (the 14 rows' own radix) the limbs of a * 2^8 ARE the R'-form of a's value (x R 2^8 = x R'),
+// and a product's 14 output limbs feed the next product directly.  Values are not reduced between
+// products: for inputs below 2^390 the output (ab + mp) / R' is below 2^388 + p, so every limb stays
+// below 2^28 and the column bounds of fp_mul28 / fp_sqr28 hold.  The end converts back with one
+// product by R mod p (r R / R' = r / 2^8 = x^e R), repacks and reduces once.
+#ifndef LB_POW28
+#define LB_POW28 1  // 0: the chains through fp_mul28 / fp_sqr28 (A/B builds)
+#endif
+struct fp28 {
+  uint32_t l[14];
+};
+LB_HD fp28 fp28_mul_raw(const fp28& a, const fp28& b) {
+  const uint32_t P28[14] = {LB_P28_0, LB_P28_1, LB_P28_2, LB_P28_3, LB_P28_4,  LB_P28_5,  LB_P28_6,
+                            LB_P28_7, LB_P28_8, LB_P28_9, LB_P28_10, LB_P28_11, LB_P28_12, LB_P28_13};
+  uint64_t acc[28];
+  LB_UNROLL for (int k = 0; k < 28; k++) acc[k] = 0;
+  LB_UNROLL for (int i = 0; i < 14; i++) {
+    LB_UNROLL for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)a.l[i] * b.l[j];
+    const uint32_t m = ((uint32_t)acc[i] * LB_PINV28) & 0x0fffffffu;
+    LB_UNROLL for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;
+  }
+  fp28 r;
+  LB_UNROLL for (int k = 0; k < 13; k++) {
+    r.l[k] = (uint32_t)acc[14 + k] & 0x0fffffffu;
+    acc[15 + k] += acc[14 + k] >> 28;
+  }
+  r.l[13] = (uint32_t)acc[27];
+  return r;
+}
+LB_HD fp28 fp28_sqr_raw(const fp28& a) {
+  const uint32_t P28[14] = {LB_P28_0, LB_P28_1, LB_P28_2, LB_P28_3, LB_P28_4,  LB_P28_5,  LB_P28_6,
+                            LB_P28_7, LB_P28_8, LB_P28_9, LB_P28_10, LB_P28_11, LB_P28_12, LB_P28_13};
+  uint32_t D[14];
+  LB_UNROLL for (int k = 0; k < 14; k++) D[k] = a.l[k] << 1;
+  uint64_t acc[28];
+  LB_UNROLL for (int k = 0; k < 28; k++) acc[k] = 0;
+  LB_UNROLL for (int i = 0; i < 14; i++) {
+    acc[2 * i] += (uint64_t)a.l[i] * a.l[i];
+    LB_UNROLL for (int j = i + 1; j < 14; j++) acc[i + j] += (uint64_t)D[i] * a.l[j];
+  }
+  LB_UNROLL for (int i = 0; i < 14; i++) {
+    const uint32_t m = ((uint32_t)acc[i] * LB_PINV28) & 0x0fffffffu;
+    LB_UNROLL for (int j = 0; j < 14; j++) acc[i + j] += (uint64_t)m * P28[j];
+    acc[i + 1] += acc[i] >> 28;
+  }
+  fp28 r;
+  LB_UNROLL for (int k = 0; k < 13; k++) {
+    r.l[k] = (uint32_t)acc[14 + k] & 0x0fffffffu;
+    acc[15 + k] += acc[14 + k] >> 28;
+  }
+  r.l[13] = (uint32_t)acc[27];
+  return r;
+}
+LB_HD fp28 fp28_mul(const fp28& a, const fp28& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+  const fp28 r = fp28_mul_raw(a, b);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+#else
+  return fp28_mul_raw(a, b);
+#endif
+}
+LB_HD fp28 fp28_sqr(const fp28& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+  const fp28 r = fp28_sqr_raw(a);
+  __builtin_amdgcn_sched_barrier(0);
+  return r;
+#else
+  return fp28_sqr_raw(a);
+#endif
+}
+LB_HD fp28 lb_tab8_28(const fp28* t, uint32_t k) {
+  switch (k) {
+    case 0: return t[0];
+    case 1: return t[1];
+    case 2: return t[2];
+    case 3: return t[3];
+    case 4: return t[4];
+    case 5: return t[5];
+    case 6: return t[6];
+    default: return t[7];
+  }
+}
+LB_HD fp fp_pow_const_28(const fp& a, const uint32_t* e, int top_bit) {
+  fp28 tab[8];
+  tab[0].l[0] = (a.v[0] << 8) & 0x0fffffffu;  // the limbs of a * 2^8: a's value in R'-form
+  LB_UNROLL for (int k = 1; k < 14; k++) tab[0].l[k] = lb_bits28(a.v, 28 * k - 8);
+  const fp28 a2 = fp28_sqr(tab[0]);
+  LB_UNROLL for (int k = 1; k < 8; k++) tab[k] = fp28_mul(tab[k - 1], a2);
+  auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
+  fp28 r = tab[0];
+  bool first = true;
+  int i = top_bit;
+  while (i >= 0) {
+    if (!bit(i)) {
+      if (!first) r = fp28_sqr(r);
+      i--;
+      continue;
+    }
+    int j = i - 3 > 0 ? i - 3 : 0;
+    while (!bit(j)) j++;
+    uint32_t val = 0;
+    for (int k = i; k >= j; k--) val = (val << 1) | bit(k);
+    if (first) {
+      r = lb_tab8_28(tab, val >> 1);
+      first = false;
+    } else {
+      for (int k = i; k >= j; k--) r = fp28_sqr(r);
+      r = fp28_mul(r, lb_tab8_28(tab, val >> 1));
+    }
+    i = j - 1;
+  }
+  // back to R-form: r * (R mod p) / R' = r / 2^8, below 2p; repack and reduce once
+  const fp one = fp_one();
+  fp28 c;
+  LB_UNROLL for (int k = 0; k < 14; k++) c.l[k] = lb_bits28(one.v, 28 * k);
+  const fp28 t = fp28_mul(r, c);
+  uint32_t o[12];
+  LB_UNROLL for (int w = 0; w < 12; w++) {
+    const int l = (32 * w) / 28, s = 32 * w - 28 * l;
+    o[w] = (t.l[l] >> s) | (t.l[l + 1] << (28 - s));
+  }
+  return fp_reduce_once(o, 0u);
+}
+
 template <bool kInlMul = false>
 LB_HD fp fp_pow_const_i(fp a, const uint32_t* e, int top_bit) {
+  if constexpr (kInlMul && LB_POW28) return fp_pow_const_28(a, e, top_bit);
   auto mul = [](const fp& x, const fp& y) { return kInlMul ? fp_mul_inl(x, y) : fp_mul(x, y); };
   auto sqr = [](const fp& x) { return kInlMul ? fp_sqr_inl(x) : fp_sqr(x); };
   fp tab[8];
