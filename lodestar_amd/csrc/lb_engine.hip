@@ -279,8 +279,9 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   while (getrandom(&e->msg_key, 8, 0) != 8) {
   }
   // s1 carries the latency-bound chain (grouping, per-root hashing and Miller loops, the root
-  // check, the invalid-set search); LB_S1_PRIORITY=1 gives it the device's highest stream priority
-  // so its few-wave kernels are dispatched ahead of the other batches' wide ones
+  // check, the invalid-set search), created at the least stream priority as measured: the
+  // greatest priority for it cost the headline 2-3 % and did not help the search (round 3,
+  // profiles/r3_search_split_ab.txt)
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
@@ -295,9 +296,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
-  const char* pv = getenv("LB_S1_PRIORITY");
-  const int s1_prio = (pv && atoi(pv) != 0) ? prio_greatest : prio_least;
-  if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, s1_prio) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess) {
