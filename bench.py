@@ -72,7 +72,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pubkey-bytes", action="store_true", help="ship 96-byte pubkeys instead of table indices")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: the host's cores as the reference pool counts them, "
+                         "os.cpus().length in multithread/poolSize.ts:7 -> host_cores())")
     ap.add_argument("--no-distinct", action="store_true",
                     help="skip the secondary measurement with every signing root distinct (c3_distinct)")
     ap.add_argument("--no-extra", action="store_true",
@@ -82,6 +84,23 @@ def parse():
     ap.add_argument("--dropin-engines", type=int, default=4)
     ap.add_argument("--dropin-rounds", type=int, default=10, help="drop-in leg: timed rounds (median reported)")
     return ap.parse_args()
+
+
+def host_cores():
+    """The CPUs this process may run on, as the reference pool sizes itself (poolSize.ts:7,
+    os.cpus().length), bounded by the cgroup CPU quota when one is set (threads beyond the quota
+    only time-slice).  Returns (threads, detail)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return n, {"sched_getaffinity": aff, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count()}
 
 
 def relaunch_distributed(a):
@@ -425,6 +444,9 @@ def signing_roots_leg():
 
 def main():
     a = parse()
+    cores_detail = None
+    if a.cpu_threads <= 0:
+        a.cpu_threads, cores_detail = host_cores()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_distributed(a))
@@ -571,6 +593,7 @@ def main():
             from oracle.cpu_pool import time_c1, time_cpu_pool
             cpu = time_cpu_pool(wl.packed, seconds=a.cpu_seconds, threads=a.cpu_threads,
                                 batchable=a.workload.startswith("c3"))
+            cpu["host_cores"] = cores_detail or {"cpu_threads_flag": a.cpu_threads}
             if wc1 is not None:
                 cpu_c1 = time_c1(wc1.packed)
         except Exception as e:  # reported, never fatal

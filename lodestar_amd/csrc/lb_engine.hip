@@ -324,14 +324,18 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   // (Not when the one-lane Miller form is disabled, LB_MILLER_FORM=g8: the queue then never needs
   // that private segment, and every queue's scratch counts against one per-process pool.)
   if (e->miller_form != 2) {
-    std::lock_guard<std::mutex> lk(g_engine_mu);
-    if (e->n_u.ensure(4) != hipSuccess || hipMemsetAsync(e->n_u.p, 0, 4, e->stream) != hipSuccess) {
-      lb_engine_destroy(e);
-      return LB_ERR_DEVICE;
+    // the lock covers only the dispatch: lb_engine_destroy takes it again on the error path
+    bool ok;
+    {
+      std::lock_guard<std::mutex> lk(g_engine_mu);
+      ok = e->n_u.ensure(4) == hipSuccess && hipMemsetAsync(e->n_u.p, 0, 4, e->stream) == hipSuccess;
+      if (ok) {
+        hipLaunchKernelGGL(k_miller_lane, dim3(4096), dim3(LB_TPB), 0, e->stream, 0u, 1u, e->n_u.as<uint32_t>(),
+                           nullptr, nullptr, nullptr, nullptr);
+        ok = hipStreamSynchronize(e->stream) == hipSuccess;
+      }
     }
-    hipLaunchKernelGGL(k_miller_lane, dim3(4096), dim3(LB_TPB), 0, e->stream, 0u, 1u, e->n_u.as<uint32_t>(), nullptr,
-                       nullptr, nullptr, nullptr);
-    if (hipStreamSynchronize(e->stream) != hipSuccess) {
+    if (!ok) {
       lb_engine_destroy(e);
       return LB_ERR_DEVICE;
     }

@@ -1,14 +1,15 @@
 "use strict";
 /**
  * Signing-root production for the TypeScript host (SURVEY.md §8(f) row 2): the signature sets of
- * a capella block with their signing roots hashed on the GPU.
+ * a phase0 / altair / bellatrix / capella block with their signing roots hashed on the GPU.
  *
- * Mirrors getBlockSignatureSets (packages/state-transition/src/signatureSets/index.ts:64-111):
+ * Mirrors getBlockSignatureSets (packages/state-transition/src/signatureSets/index.ts:26-72):
  * randao (randao.ts), proposer slashings (proposerSlashings.ts), attester slashings
  * (attesterSlashings.ts), attestations (indexedAttestation.ts), voluntary exits
- * (voluntaryExits.ts), proposer (proposer.ts), the sync aggregate
- * (block/processSyncCommittee.ts:58-111) and BLS-to-execution changes (blsToExecutionChange.ts),
- * in that order.  Each root is computeSigningRoot(type, value, domain) =
+ * (voluntaryExits.ts), proposer (proposer.ts, the BeaconBlock type of the block's fork), then by
+ * config.getForkSeq(slot) the sync aggregate from altair on (block/processSyncCommittee.ts:58-111,
+ * which throws "Empty sync committee signature is not infinity" for an empty participation with
+ * another signature) and BLS-to-execution changes from capella on (blsToExecutionChange.ts).  Each root is computeSigningRoot(type, value, domain) =
  * hash_tree_root(SigningData{hash_tree_root(value), domain}) (src/util/signingRoot.ts:7-13).
  *
  * The SSZ containers (beacon-API JSON, the same objects lodestar_amd/signing_roots.py walks) are
@@ -31,6 +32,26 @@ const DOMAIN_RANDAO = Uint8Array.from([2, 0, 0, 0]);
 const DOMAIN_VOLUNTARY_EXIT = Uint8Array.from([4, 0, 0, 0]);
 const DOMAIN_SYNC_COMMITTEE = Uint8Array.from([7, 0, 0, 0]);
 const DOMAIN_BLS_TO_EXECUTION_CHANGE = Uint8Array.from([10, 0, 0, 0]);
+const MAX_VALIDATORS_PER_COMMITTEE = 2048;
+/** ForkSeq (packages/params/src/forkName.ts) */
+const ForkSeq = {phase0: 0, altair: 1, bellatrix: 2, capella: 3};
+/** mainnet fork epochs (config/src/chainConfig/presets/mainnet.ts:34-42; capella unscheduled there) */
+const MAINNET_FORK_EPOCHS = {altair: 74240, bellatrix: 144896, capella: Infinity};
+/** G2_POINT_AT_INFINITY (params/src/index.ts) */
+const G2_POINT_AT_INFINITY = (() => {
+  const b = new Uint8Array(96);
+  b[0] = 0xc0;
+  return b;
+})();
+
+/** slot -> ForkSeq for the given fork epochs (config.getForkSeq) */
+function forkSchedule(epochs) {
+  const e = Object.assign({altair: Infinity, bellatrix: Infinity, capella: Infinity}, epochs);
+  return (slot) => {
+    const ep = Math.floor(Number(slot) / SLOTS_PER_EPOCH);
+    return ep >= e.capella ? ForkSeq.capella : ep >= e.bellatrix ? ForkSeq.bellatrix : ep >= e.altair ? ForkSeq.altair : ForkSeq.phase0;
+  };
+}
 
 /** hash_tree_root of `parts` (32-byte chunks or Trees) padded to 2^depth leaves, mix = length or null */
 class Tree {
@@ -88,6 +109,19 @@ function bytesN(b) {
   return ch.length === 1 ? ch[0] : new Tree(ch, ceilLog2(ch.length));
 }
 
+/** List[uint64, limit]: values packed 4 per 32-byte chunk, limit ceil(8*limit/32) chunks */
+function uint64List(values, limit) {
+  const raw = new Uint8Array(8 * values.length);
+  values.forEach((x, i) => {
+    let v = BigInt(x);
+    for (let j = 0; j < 8; j++) {
+      raw[8 * i + j] = Number(v & 0xffn);
+      v >>= 8n;
+    }
+  });
+  return new Tree(raw.length ? pack(raw) : [], ceilLog2(Math.ceil((8 * limit) / 32)), values.length);
+}
+
 function byteList(b, limit) {
   return new Tree(b.length ? pack(b) : [], ceilLog2(Math.ceil(limit / 32)), b.length);
 }
@@ -137,7 +171,7 @@ const checkpoint = (c) => container([uint64(c.epoch), hx(c.root)]);
 const attestationData = (d) =>
   container([uint64(d.slot), uint64(d.index), hx(d.beacon_block_root), checkpoint(d.source), checkpoint(d.target)]);
 const indexedAttestation = (a) =>
-  container([listOf(a.attesting_indices.map(uint64), 2048), attestationData(a.data), bytesN(hx(a.signature))]);
+  container([uint64List(a.attesting_indices, MAX_VALIDATORS_PER_COMMITTEE), attestationData(a.data), bytesN(hx(a.signature))]);
 const attestation = (a) =>
   container([bitlist(bitsFromBitlistHex(a.aggregation_bits), 2048), attestationData(a.data), bytesN(hx(a.signature))]);
 const blockHeader = (h) =>
@@ -148,15 +182,14 @@ const blsToExecutionChange = (c) =>
   container([uint64(c.validator_index), bytesN(hx(c.from_bls_pubkey)), bytesN(hx(c.to_execution_address))]);
 const withdrawal = (w) => container([uint64(w.index), uint64(w.validator_index), bytesN(hx(w.address)), uint64(w.amount)]);
 
-function executionPayloadCapella(p) {
-  return container([
-    hx(p.parent_hash), bytesN(hx(p.fee_recipient)), hx(p.state_root), hx(p.receipts_root), bytesN(hx(p.logs_bloom)),
-    hx(p.prev_randao), uint64(p.block_number), uint64(p.gas_limit), uint64(p.gas_used), uint64(p.timestamp),
-    byteList(hx(p.extra_data), 32), uint256(p.base_fee_per_gas), hx(p.block_hash),
-    listOf(p.transactions.map((t) => byteList(hx(t), 2 ** 30)), 2 ** 20),
-    listOf(p.withdrawals.map(withdrawal), 16),
-  ]);
-}
+const executionPayloadFields = (p) => [
+  hx(p.parent_hash), bytesN(hx(p.fee_recipient)), hx(p.state_root), hx(p.receipts_root), bytesN(hx(p.logs_bloom)),
+  hx(p.prev_randao), uint64(p.block_number), uint64(p.gas_limit), uint64(p.gas_used), uint64(p.timestamp),
+  byteList(hx(p.extra_data), 32), uint256(p.base_fee_per_gas), hx(p.block_hash),
+  listOf(p.transactions.map((t) => byteList(hx(t), 2 ** 30)), 2 ** 20),
+];
+const executionPayloadBellatrix = (p) => container(executionPayloadFields(p));
+const executionPayloadCapella = (p) => container([...executionPayloadFields(p), listOf(p.withdrawals.map(withdrawal), 16)]);
 
 function deposit(d) {
   const data = d.data;
@@ -164,9 +197,13 @@ function deposit(d) {
     container([bytesN(hx(data.pubkey)), hx(data.withdrawal_credentials), uint64(data.amount), bytesN(hx(data.signature))])]);
 }
 
-function beaconBlockBodyCapella(b) {
-  const sa = b.sync_aggregate;
-  return container([
+/**
+ * BeaconBlockBody of `fork` (types/src/{phase0,altair,bellatrix,capella}/sszTypes.ts): phase0's 8
+ * fields, + sync_aggregate (altair), + execution_payload (bellatrix), capella's payload with
+ * withdrawals + bls_to_execution_changes
+ */
+function beaconBlockBody(b, fork) {
+  const fields = [
     bytesN(hx(b.randao_reveal)),
     container([hx(b.eth1_data.deposit_root), uint64(b.eth1_data.deposit_count), hx(b.eth1_data.block_hash)]),
     hx(b.graffiti),
@@ -175,14 +212,24 @@ function beaconBlockBodyCapella(b) {
     listOf(b.attestations.map(attestation), 128),
     listOf(b.deposits.map(deposit), 16),
     listOf(b.voluntary_exits.map((e) => container([voluntaryExit(e.message), bytesN(hx(e.signature))])), 16),
-    container([bitvector(bitsFromBitvectorHex(sa.sync_committee_bits, SYNC_COMMITTEE_SIZE)), bytesN(hx(sa.sync_committee_signature))]),
-    executionPayloadCapella(b.execution_payload),
-    listOf(b.bls_to_execution_changes.map((c) => container([blsToExecutionChange(c.message), bytesN(hx(c.signature))])), 16),
-  ]);
+  ];
+  if (fork >= ForkSeq.altair) {
+    const sa = b.sync_aggregate;
+    fields.push(container([bitvector(bitsFromBitvectorHex(sa.sync_committee_bits, SYNC_COMMITTEE_SIZE)), bytesN(hx(sa.sync_committee_signature))]));
+  }
+  if (fork === ForkSeq.bellatrix) fields.push(executionPayloadBellatrix(b.execution_payload));
+  if (fork >= ForkSeq.capella) {
+    fields.push(executionPayloadCapella(b.execution_payload));
+    fields.push(listOf(b.bls_to_execution_changes.map((c) => container([blsToExecutionChange(c.message), bytesN(hx(c.signature))])), 16));
+  }
+  return container(fields);
 }
 
-const beaconBlockCapella = (m) =>
-  container([uint64(m.slot), uint64(m.proposer_index), hx(m.parent_root), hx(m.state_root), beaconBlockBodyCapella(m.body)]);
+/** BeaconBlock of `fork` (config.getForkTypes(slot).BeaconBlock, proposer.ts:22-24) */
+const beaconBlock = (m, fork) =>
+  container([uint64(m.slot), uint64(m.proposer_index), hx(m.parent_root), hx(m.state_root), beaconBlockBody(m.body, fork)]);
+const beaconBlockBodyCapella = (b) => beaconBlockBody(b, ForkSeq.capella);
+const beaconBlockCapella = (m) => beaconBlock(m, ForkSeq.capella);
 
 const signingTree = (obj, domain) => container([obj, domain]);
 
@@ -202,7 +249,8 @@ function computeDomain(domainType, forkVersion, genesisValidatorsRoot) {
  * index2pubkey, beacon committees and the current sync committee.
  * @typedef {{genesisValidatorsRoot: Uint8Array, forkPreviousVersion: Uint8Array, forkCurrentVersion: Uint8Array,
  *   forkEpoch: number, slot?: number, pubkey: (i: number) => any, beaconCommittee: (slot: number, index: number) => number[],
- *   syncCommittee: () => any[], keyFromBytes?: (b48: Uint8Array) => any}} StateView
+ *   syncCommittee: () => any[], keyFromBytes?: (b48: Uint8Array) => any, forkSeq?: (slot: number) => number}} StateView
+ * (forkSeq: config.getForkSeq; capella for every slot when absent, see forkSchedule)
  */
 function domainOf(state, domainType, epoch) {
   const key = `${Buffer.from(domainType).toString("hex")}:${epoch < state.forkEpoch ? "p" : "c"}`;
@@ -217,8 +265,27 @@ function domainOf(state, domainType, epoch) {
 }
 
 /**
- * getBlockSignatureSets for one capella SignedBeaconBlock (beacon-API JSON).  Signing roots are
- * left as Trees; resolve() hashes the trees of many blocks together.
+ * getSyncCommitteeSignatureSet (block/processSyncCommittee.ts:58-111): null for an empty
+ * participation with the infinity signature, the reference's Error for any other signature
+ */
+function getSyncCommitteeSignatureSet(state, m) {
+  const sa = m.body.sync_aggregate;
+  const sig = hx(sa.sync_committee_signature);
+  const sbits = bitsFromBitvectorHex(sa.sync_committee_bits, SYNC_COMMITTEE_SIZE);
+  const keys = state.syncCommittee().filter((_, k) => sbits[k]);
+  if (keys.length === 0) {
+    if (Buffer.from(sig).equals(Buffer.from(G2_POINT_AT_INFINITY))) return null;
+    throw Error("Empty sync committee signature is not infinity");
+  }
+  const prev = Math.max(Number(m.slot), 1) - 1;
+  return {name: "sync_aggregate", type: "aggregate", pubkeys: keys,
+    signingRoot: signingTree(hx(m.parent_root), domainOf(state, DOMAIN_SYNC_COMMITTEE, Math.floor(prev / SLOTS_PER_EPOCH))),
+    signature: sig};
+}
+
+/**
+ * getBlockSignatureSets for one SignedBeaconBlock of any fork up to capella (beacon-API JSON).
+ * Signing roots are left as Trees; resolve() hashes the trees of many blocks together.
  * @returns {{name: string, type: "single"|"aggregate", pubkey?: any, pubkeys?: any[], signingRoot: Tree|Uint8Array, signature: Uint8Array}[]}
  */
 function getBlockSignatureSets(state, signedBlock, opts) {
@@ -228,6 +295,7 @@ function getBlockSignatureSets(state, signedBlock, opts) {
   const epoch = Math.floor(slot / SLOTS_PER_EPOCH);
   const stateEpoch = Math.floor((state.slot === undefined ? slot : Number(state.slot)) / SLOTS_PER_EPOCH);
   const keyFromBytes = state.keyFromBytes || ((k) => k);
+  const fork = state.forkSeq ? state.forkSeq(slot) : ForkSeq.capella;
   const single = (name, pk, root, sig) => ({name, type: "single", pubkey: pk, signingRoot: root, signature: sig});
   const sets = [];
   sets.push(single("randao", state.pubkey(Number(m.proposer_index)), signingTree(uint64(epoch), domainOf(state, DOMAIN_RANDAO, epoch)),
@@ -259,16 +327,12 @@ function getBlockSignatureSets(state, signedBlock, opts) {
       signingTree(voluntaryExit(e.message), domainOf(state, DOMAIN_VOLUNTARY_EXIT, Number(e.message.epoch))), hx(e.signature)));
   if (!(opts && opts.skipProposerSignature))
     sets.push(single("proposer", state.pubkey(Number(m.proposer_index)),
-      signingTree(beaconBlockCapella(m), domainOf(state, DOMAIN_BEACON_PROPOSER, epoch)), hx(signedBlock.signature)));
-  const sa = b.sync_aggregate;
-  const sbits = bitsFromBitvectorHex(sa.sync_committee_bits, SYNC_COMMITTEE_SIZE);
-  const keys = state.syncCommittee().filter((_, k) => sbits[k]);
-  if (keys.length) {
-    const prev = Math.max(slot, 1) - 1;
-    sets.push({name: "sync_aggregate", type: "aggregate", pubkeys: keys,
-      signingRoot: signingTree(hx(m.parent_root), domainOf(state, DOMAIN_SYNC_COMMITTEE, Math.floor(prev / SLOTS_PER_EPOCH))),
-      signature: hx(sa.sync_committee_signature)});
+      signingTree(beaconBlock(m, fork), domainOf(state, DOMAIN_BEACON_PROPOSER, epoch)), hx(signedBlock.signature)));
+  if (fork >= ForkSeq.altair) {
+    const sync = getSyncCommitteeSignatureSet(state, m);
+    if (sync) sets.push(sync);
   }
+  if (fork < ForkSeq.capella) return sets;
   for (const c of b.bls_to_execution_changes)
     sets.push(single("bls_to_execution_change", keyFromBytes(hx(c.message.from_bls_pubkey)),
       signingTree(blsToExecutionChange(c.message), domainOf(state, DOMAIN_BLS_TO_EXECUTION_CHANGE, stateEpoch)), hx(c.signature)));
@@ -334,7 +398,14 @@ function resolve(sets, merkleize) {
 
 module.exports = {
   Tree,
+  ForkSeq,
+  MAINNET_FORK_EPOCHS,
+  G2_POINT_AT_INFINITY,
+  forkSchedule,
   getBlockSignatureSets,
+  getSyncCommitteeSignatureSet,
+  beaconBlock,
+  beaconBlockBody,
   evaluate,
   resolve,
   gpuMerkleizer,

@@ -1,10 +1,13 @@
 """Signing-root production on the GPU: the signature sets of a block.
 
-Mirrors getBlockSignatureSets (packages/state-transition/src/signatureSets/index.ts:64-111) for
-capella blocks: proposer (signatureSets/proposer.ts), randao (randao.ts), proposer and attester
-slashings (proposerSlashings.ts, attesterSlashings.ts), attestations (indexedAttestation.ts),
-voluntary exits (voluntaryExits.ts), the sync aggregate (block/processSyncCommittee.ts:58-111)
-and BLS-to-execution changes (blsToExecutionChange.ts).  Each set's signing root is
+Mirrors getBlockSignatureSets (packages/state-transition/src/signatureSets/index.ts:26-72) for
+phase0, altair, bellatrix and capella blocks, dispatched on the fork of the block's slot like
+the reference (config.getForkSeq(slot), index.ts:46-70): proposer (signatureSets/proposer.ts,
+the fork's BeaconBlock type), randao (randao.ts), proposer and attester slashings
+(proposerSlashings.ts, attesterSlashings.ts), attestations (indexedAttestation.ts), voluntary
+exits (voluntaryExits.ts), the sync aggregate from altair on (block/processSyncCommittee.ts:58-111,
+including its "Empty sync committee signature is not infinity" rejection) and BLS-to-execution
+changes from capella on (blsToExecutionChange.ts).  Each set's signing root is
 computeSigningRoot(type, value, domain) = hash_tree_root(SigningData{hash_tree_root(value),
 domain}) (src/util/signingRoot.ts:7-13).
 
@@ -26,6 +29,7 @@ import numpy as np
 
 SLOTS_PER_EPOCH = 32
 SYNC_COMMITTEE_SIZE = 512
+MAX_VALIDATORS_PER_COMMITTEE = 2048
 NO_MIX = 0xFFFFFFFFFFFFFFFF
 
 DOMAIN_BEACON_PROPOSER = bytes.fromhex("00000000")
@@ -34,6 +38,24 @@ DOMAIN_RANDAO = bytes.fromhex("02000000")
 DOMAIN_VOLUNTARY_EXIT = bytes.fromhex("04000000")
 DOMAIN_SYNC_COMMITTEE = bytes.fromhex("07000000")
 DOMAIN_BLS_TO_EXECUTION_CHANGE = bytes.fromhex("0a000000")
+
+# ForkSeq (packages/params/src/forkName.ts)
+FORK_PHASE0, FORK_ALTAIR, FORK_BELLATRIX, FORK_CAPELLA = range(4)
+FAR_FUTURE = 2 ** 64 - 1
+# mainnet fork epochs (config/src/chainConfig/presets/mainnet.ts:34-42; capella unscheduled there)
+MAINNET_FORK_EPOCHS = (74240, 144896, FAR_FUTURE)
+# G2_POINT_AT_INFINITY (params/src/index.ts): the compressed infinity flag byte, then zeros
+G2_POINT_AT_INFINITY = bytes([0xC0]) + bytes(95)
+
+
+def fork_schedule(altair_epoch: int, bellatrix_epoch: int = FAR_FUTURE,
+                  capella_epoch: int = FAR_FUTURE) -> Callable[[int], int]:
+    """slot -> ForkSeq, as config.getForkSeq(slot) for the given fork epochs."""
+    def seq(slot: int) -> int:
+        ep = int(slot) // SLOTS_PER_EPOCH
+        return (FORK_CAPELLA if ep >= capella_epoch else FORK_BELLATRIX if ep >= bellatrix_epoch
+                else FORK_ALTAIR if ep >= altair_epoch else FORK_PHASE0)
+    return seq
 
 
 # ------------------------------------------------------------------ merkle trees
@@ -136,6 +158,12 @@ def bytes_n(b: bytes) -> Node:
     return ch[0] if len(ch) == 1 else Tree(ch, _ceil_log2(len(ch)))
 
 
+def uint64_list(values: Sequence[int], limit: int) -> Tree:
+    """List[uint64, limit]: basic values packed 4 per 32-byte chunk, limit ceil(8*limit/32) chunks."""
+    raw = b"".join(int(v).to_bytes(8, "little") for v in values)
+    return Tree(pack(raw), _ceil_log2((8 * limit + 31) // 32), mix=len(values))
+
+
 def byte_list(b: bytes, limit: int) -> Tree:
     return Tree(pack(b), _ceil_log2((limit + 31) // 32), mix=len(b))
 
@@ -184,8 +212,8 @@ def attestation_data(d) -> Tree:
 
 
 def indexed_attestation(a) -> Tree:
-    return container([list_of([uint64(i) for i in a["attesting_indices"]], 2048), attestation_data(a["data"]),
-                      bytes_n(hx(a["signature"]))])
+    return container([uint64_list([int(i) for i in a["attesting_indices"]], MAX_VALIDATORS_PER_COMMITTEE),
+                      attestation_data(a["data"]), bytes_n(hx(a["signature"]))])
 
 
 def attestation(a) -> Tree:
@@ -215,19 +243,27 @@ def withdrawal(w) -> Tree:
     return container([uint64(w["index"]), uint64(w["validator_index"]), bytes_n(hx(w["address"])), uint64(w["amount"])])
 
 
+def _execution_payload_fields(p) -> List[Node]:
+    return [hx(p["parent_hash"]), bytes_n(hx(p["fee_recipient"])), hx(p["state_root"]), hx(p["receipts_root"]),
+            bytes_n(hx(p["logs_bloom"])), hx(p["prev_randao"]), uint64(p["block_number"]), uint64(p["gas_limit"]),
+            uint64(p["gas_used"]), uint64(p["timestamp"]), byte_list(hx(p["extra_data"]), 32),
+            uint256(int(p["base_fee_per_gas"])), hx(p["block_hash"]),
+            list_of([byte_list(hx(t), 2 ** 30) for t in p["transactions"]], 2 ** 20)]
+
+
+def execution_payload_bellatrix(p) -> Tree:
+    return container(_execution_payload_fields(p))
+
+
 def execution_payload_capella(p) -> Tree:
-    return container([
-        hx(p["parent_hash"]), bytes_n(hx(p["fee_recipient"])), hx(p["state_root"]), hx(p["receipts_root"]),
-        bytes_n(hx(p["logs_bloom"])), hx(p["prev_randao"]), uint64(p["block_number"]), uint64(p["gas_limit"]),
-        uint64(p["gas_used"]), uint64(p["timestamp"]), byte_list(hx(p["extra_data"]), 32),
-        uint256(int(p["base_fee_per_gas"])), hx(p["block_hash"]),
-        list_of([byte_list(hx(t), 2 ** 30) for t in p["transactions"]], 2 ** 20),
-        list_of([withdrawal(w) for w in p["withdrawals"]], 16)])
+    return container(_execution_payload_fields(p) + [list_of([withdrawal(w) for w in p["withdrawals"]], 16)])
 
 
-def beacon_block_body_capella(b) -> Tree:
-    sa = b["sync_aggregate"]
-    return container([
+def beacon_block_body(b, fork: int) -> Tree:
+    """BeaconBlockBody of `fork` (types/src/{phase0,altair,bellatrix,capella}/sszTypes.ts): phase0's
+    8 fields, + sync_aggregate (altair), + execution_payload (bellatrix), capella's payload with
+    withdrawals + bls_to_execution_changes."""
+    fields: List[Node] = [
         bytes_n(hx(b["randao_reveal"])),
         container([hx(b["eth1_data"]["deposit_root"]), uint64(b["eth1_data"]["deposit_count"]),
                    hx(b["eth1_data"]["block_hash"])]),
@@ -239,12 +275,18 @@ def beacon_block_body_capella(b) -> Tree:
         list_of([attestation(a) for a in b["attestations"]], 128),
         list_of([_deposit(d) for d in b["deposits"]], 16),
         list_of([container([voluntary_exit(e["message"]), bytes_n(hx(e["signature"]))])
-                 for e in b["voluntary_exits"]], 16),
-        container([bitvector(bits_from_bitvector_hex(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)),
-                   bytes_n(hx(sa["sync_committee_signature"]))]),
-        execution_payload_capella(b["execution_payload"]),
-        list_of([container([bls_to_execution_change(c["message"]), bytes_n(hx(c["signature"]))])
-                 for c in b["bls_to_execution_changes"]], 16)])
+                 for e in b["voluntary_exits"]], 16)]
+    if fork >= FORK_ALTAIR:
+        sa = b["sync_aggregate"]
+        fields.append(container([bitvector(bits_from_bitvector_hex(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)),
+                                 bytes_n(hx(sa["sync_committee_signature"]))]))
+    if fork == FORK_BELLATRIX:
+        fields.append(execution_payload_bellatrix(b["execution_payload"]))
+    if fork >= FORK_CAPELLA:
+        fields.append(execution_payload_capella(b["execution_payload"]))
+        fields.append(list_of([container([bls_to_execution_change(c["message"]), bytes_n(hx(c["signature"]))])
+                               for c in b["bls_to_execution_changes"]], 16))
+    return container(fields)
 
 
 def _deposit(d) -> Tree:
@@ -254,9 +296,18 @@ def _deposit(d) -> Tree:
                                  uint64(data["amount"]), bytes_n(hx(data["signature"]))])])
 
 
-def beacon_block_capella(m) -> Tree:
+def beacon_block(m, fork: int) -> Tree:
+    """BeaconBlock of `fork` (config.getForkTypes(slot).BeaconBlock, proposer.ts:22-24)."""
     return container([uint64(m["slot"]), uint64(m["proposer_index"]), hx(m["parent_root"]), hx(m["state_root"]),
-                      beacon_block_body_capella(m["body"])])
+                      beacon_block_body(m["body"], fork)])
+
+
+def beacon_block_body_capella(b) -> Tree:
+    return beacon_block_body(b, FORK_CAPELLA)
+
+
+def beacon_block_capella(m) -> Tree:
+    return beacon_block(m, FORK_CAPELLA)
 
 
 def signing_tree(obj: Node, domain: bytes) -> Tree:
@@ -284,6 +335,8 @@ class StateView:
     # bls.PublicKey.fromBytes(bytes48, affine, true) for keys carried in the block itself
     # (BLS-to-execution changes, blsToExecutionChange.ts:30)
     key_from_bytes: Callable[[bytes], object] = lambda b: b
+    # config.getForkSeq(slot): capella for every slot unless a schedule is given (fork_schedule)
+    fork_seq: Callable[[int], int] = lambda slot: FORK_CAPELLA
 
     def domain(self, domain_type: bytes, epoch: int) -> bytes:
         """config.getDomain(state.slot, type, messageSlot) (config/src/genesisConfig/index.ts:27-54):
@@ -302,13 +355,16 @@ class BlockSet:
 
 
 def block_signature_sets(signed_block, state: StateView, skip_proposer_signature: bool = False) -> List[BlockSet]:
-    """getBlockSignatureSets (signatureSets/index.ts:64-111) for one capella SignedBeaconBlock
-    (JSON as served by the beacon API), in the reference's order: randao, proposer slashings,
-    attester slashings, attestations, voluntary exits, proposer, sync aggregate, BLS-to-execution
-    changes.  Signing roots are left as trees: evaluate() hashes the trees of many blocks together."""
+    """getBlockSignatureSets (signatureSets/index.ts:26-72) for one SignedBeaconBlock of any fork
+    up to capella (JSON as served by the beacon API), in the reference's order: randao, proposer
+    slashings, attester slashings, attestations, voluntary exits, proposer, then by the fork of the
+    block's slot the sync aggregate (altair on) and BLS-to-execution changes (capella on).  Signing
+    roots are left as trees: evaluate() hashes the trees of many blocks together.  Raises
+    ValueError("Empty sync committee signature is not infinity") like processSyncCommittee.ts:93-101."""
     m = signed_block["message"]
     b = m["body"]
     slot = int(m["slot"])
+    fork = state.fork_seq(slot)
     epoch = slot // SLOTS_PER_EPOCH
     state_epoch = (slot if state.slot is None else int(state.slot)) // SLOTS_PER_EPOCH
     out: List[BlockSet] = []
@@ -349,18 +405,14 @@ def block_signature_sets(signed_block, state: StateView, skip_proposer_signature
     # proposer.ts:20 (index.ts:86-88: after the operations)
     if not skip_proposer_signature:
         out.append(BlockSet("proposer", "single", [state.pubkey(int(m["proposer_index"]))],
-                            signing_tree(beacon_block_capella(m), state.domain(DOMAIN_BEACON_PROPOSER, epoch)),
+                            signing_tree(beacon_block(m, fork), state.domain(DOMAIN_BEACON_PROPOSER, epoch)),
                             hx(signed_block["signature"])))
-    # block/processSyncCommittee.ts:58-111
-    sa = b["sync_aggregate"]
-    bits = bits_from_bitvector_hex(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)
-    keys = [k for k, bit in zip(state.sync_committee(), bits) if bit]
-    if keys:  # an empty participation needs the infinity signature instead (processSyncCommittee.ts)
-        prev = max(slot, 1) - 1
-        out.append(BlockSet("sync_aggregate", "aggregate", keys,
-                            signing_tree(hx(m["parent_root"]), state.domain(DOMAIN_SYNC_COMMITTEE,
-                                                                            prev // SLOTS_PER_EPOCH)),
-                            hx(sa["sync_committee_signature"])))
+    if fork >= FORK_ALTAIR:
+        s = sync_committee_set(m, state)
+        if s is not None:
+            out.append(s)
+    if fork < FORK_CAPELLA:
+        return out
     # blsToExecutionChange.ts:23: getDomain(state.slot, DOMAIN_BLS_TO_EXECUTION_CHANGE), i.e. the
     # fork of the state's own epoch; the key is the message's from_bls_pubkey (48 B compressed)
     for c in b["bls_to_execution_changes"]:
@@ -368,6 +420,24 @@ def block_signature_sets(signed_block, state: StateView, skip_proposer_signature
         out.append(BlockSet("bls_to_execution_change", "single", [state.key_from_bytes(hx(c["message"]["from_bls_pubkey"]))],
                             signing_tree(bls_to_execution_change(c["message"]), dom), hx(c["signature"])))
     return out
+
+
+def sync_committee_set(m, state: StateView) -> Optional[BlockSet]:
+    """getSyncCommitteeSignatureSet (block/processSyncCommittee.ts:58-111): the participants' keys
+    over the parent root; no participant -> None if the signature is G2_POINT_AT_INFINITY, else the
+    reference's error (the block is rejected)."""
+    sa = m["body"]["sync_aggregate"]
+    sig = hx(sa["sync_committee_signature"])
+    bits = bits_from_bitvector_hex(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)
+    keys = [k for k, bit in zip(state.sync_committee(), bits) if bit]
+    if not keys:
+        if sig == G2_POINT_AT_INFINITY:
+            return None
+        raise ValueError("Empty sync committee signature is not infinity")
+    prev = max(int(m["slot"]), 1) - 1
+    return BlockSet("sync_aggregate", "aggregate", keys,
+                    signing_tree(hx(m["parent_root"]), state.domain(DOMAIN_SYNC_COMMITTEE, prev // SLOTS_PER_EPOCH)),
+                    sig)
 
 
 def resolve(sets: Sequence[BlockSet], merkleize) -> List[BlockSet]:

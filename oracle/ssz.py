@@ -7,8 +7,11 @@ with @chainsafe/ssz through @lodestar/types: ssz.phase0.SigningData.hashTreeRoot
 packages/state-transition/src/util/signingRoot.ts:7-13, BeaconBlock / AttestationData roots in
 src/signatureSets/*.ts) and of the domain / committee helpers the block's signature sets need:
 compute_domain / getDomain (packages/config/src/genesisConfig/index.ts:27-54), the swap-or-not
-shuffle (state-transition/src/util/shuffle.ts), get_beacon_committee (epochContext), for the
-capella fork the devnet fixture K3 uses.  Mainnet preset constants.
+shuffle (state-transition/src/util/shuffle.ts), get_beacon_committee (epochContext).  Block
+containers for phase0 / altair / bellatrix / capella (packages/types/src/{phase0,altair,bellatrix,
+capella}/sszTypes.ts), pinned by the capella devnet fixture K3 and the first four mainnet phase0
+blocks of beacon-node/test/unit/sync/backfill/blocks.json.  Mainnet preset
+constants.
 """
 from __future__ import annotations
 
@@ -24,6 +27,7 @@ SLOTS_PER_HISTORICAL_ROOT = 8192
 EPOCHS_PER_SLASHINGS_VECTOR = 8192
 MIN_SEED_LOOKAHEAD = 1
 SYNC_COMMITTEE_SIZE = 512
+MAX_VALIDATORS_PER_COMMITTEE = 2048
 FAR_FUTURE_EPOCH = 2 ** 64 - 1
 
 DOMAIN_BEACON_PROPOSER = bytes.fromhex("00000000")
@@ -110,6 +114,12 @@ def list_of(roots: Sequence[bytes], limit: int) -> bytes:
     return mix_in_length(merkleize(roots, limit), len(roots))
 
 
+def list_of_uint64(values: Sequence[int], limit: int) -> bytes:
+    """List[uint64, limit]: basic values packed 4 per chunk, limit ceil(limit*8/32) chunks."""
+    raw = b"".join(int(v).to_bytes(8, "little") for v in values)
+    return mix_in_length(merkleize(pack(raw), (limit * 8 + 31) // 32), len(values))
+
+
 def bits_from_hex_bitlist(h: str) -> List[int]:
     """SSZ Bitlist serialisation (length marker bit) -> list of bits."""
     b = bytes.fromhex(h[2:] if h.startswith("0x") else h)
@@ -182,29 +192,76 @@ def bls_to_execution_change(c) -> bytes:
                       bytes_n(hx(c["to_execution_address"]))])
 
 
-def beacon_block_body_capella(b) -> bytes:
-    for k in ("attester_slashings", "deposits"):
-        if b[k]:
-            raise NotImplementedError(f"{k} present in the block: not needed by the fixtures")
-    sa = b["sync_aggregate"]
+def execution_payload_bellatrix(p) -> bytes:
+    txs = [byte_list(hx(t), 2 ** 30) for t in p["transactions"]]
     return container([
+        hx(p["parent_hash"]), bytes_n(hx(p["fee_recipient"])), hx(p["state_root"]), hx(p["receipts_root"]),
+        bytes_n(hx(p["logs_bloom"])), hx(p["prev_randao"]), uint64(int(p["block_number"])),
+        uint64(int(p["gas_limit"])), uint64(int(p["gas_used"])), uint64(int(p["timestamp"])),
+        byte_list(hx(p["extra_data"]), 32), uint256(int(p["base_fee_per_gas"])), hx(p["block_hash"]),
+        list_of(txs, 2 ** 20)])
+
+
+def indexed_attestation(a) -> bytes:
+    """phase0 IndexedAttestation: attesting_indices is List[ValidatorIndex, 2048] of packed uint64"""
+    return container([list_of_uint64([int(i) for i in a["attesting_indices"]], MAX_VALIDATORS_PER_COMMITTEE),
+                      attestation_data(a["data"]), bytes_n(hx(a["signature"]))])
+
+
+def attester_slashing(s) -> bytes:
+    return container([indexed_attestation(s["attestation_1"]), indexed_attestation(s["attestation_2"])])
+
+
+def deposit(d) -> bytes:
+    """phase0 Deposit: proof Vector[Bytes32, 33] + DepositData"""
+    data = d["data"]
+    return container([merkleize([hx(x) for x in d["proof"]], 33),
+                      container([bytes_n(hx(data["pubkey"])), hx(data["withdrawal_credentials"]),
+                                 uint64(int(data["amount"])), bytes_n(hx(data["signature"]))])])
+
+
+def sync_aggregate(sa) -> bytes:
+    return container([bitvector(bits_from_hex_bitvector(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)),
+                      bytes_n(hx(sa["sync_committee_signature"]))])
+
+
+FORK_PHASE0, FORK_ALTAIR, FORK_BELLATRIX, FORK_CAPELLA = range(4)
+
+
+def beacon_block_body(b, fork: int) -> bytes:
+    """BeaconBlockBody of `fork` (phase0: 8 fields, altair +sync_aggregate, bellatrix
+    +execution_payload, capella: capella payload +bls_to_execution_changes)."""
+    fields = [
         bytes_n(hx(b["randao_reveal"])), eth1_data(b["eth1_data"]), hx(b["graffiti"]),
         list_of([container([signed_block_header(s["signed_header_1"]), signed_block_header(s["signed_header_2"])])
                  for s in b["proposer_slashings"]], 16),
-        list_of([], 2), list_of([attestation(a) for a in b["attestations"]], 128),
-        list_of([], 16),
+        list_of([attester_slashing(s) for s in b["attester_slashings"]], 2),
+        list_of([attestation(a) for a in b["attestations"]], 128),
+        list_of([deposit(d) for d in b["deposits"]], 16),
         list_of([container([voluntary_exit(e["message"]), bytes_n(hx(e["signature"]))])
-                 for e in b["voluntary_exits"]], 16),
-        container([bitvector(bits_from_hex_bitvector(sa["sync_committee_bits"], SYNC_COMMITTEE_SIZE)),
-                   bytes_n(hx(sa["sync_committee_signature"]))]),
-        execution_payload_capella(b["execution_payload"]),
-        list_of([container([bls_to_execution_change(c["message"]), bytes_n(hx(c["signature"]))])
-                 for c in b["bls_to_execution_changes"]], 16)])
+                 for e in b["voluntary_exits"]], 16)]
+    if fork >= FORK_ALTAIR:
+        fields.append(sync_aggregate(b["sync_aggregate"]))
+    if fork == FORK_BELLATRIX:
+        fields.append(execution_payload_bellatrix(b["execution_payload"]))
+    if fork >= FORK_CAPELLA:
+        fields.append(execution_payload_capella(b["execution_payload"]))
+        fields.append(list_of([container([bls_to_execution_change(c["message"]), bytes_n(hx(c["signature"]))])
+                               for c in b["bls_to_execution_changes"]], 16))
+    return container(fields)
+
+
+def beacon_block(m, fork: int) -> bytes:
+    return container([uint64(int(m["slot"])), uint64(int(m["proposer_index"])), hx(m["parent_root"]),
+                      hx(m["state_root"]), beacon_block_body(m["body"], fork)])
+
+
+def beacon_block_body_capella(b) -> bytes:
+    return beacon_block_body(b, FORK_CAPELLA)
 
 
 def beacon_block_capella(m) -> bytes:
-    return container([uint64(int(m["slot"])), uint64(int(m["proposer_index"])), hx(m["parent_root"]),
-                      hx(m["state_root"]), beacon_block_body_capella(m["body"])])
+    return beacon_block(m, FORK_CAPELLA)
 
 
 def signing_root(object_root: bytes, domain: bytes) -> bytes:

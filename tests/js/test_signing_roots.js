@@ -2,6 +2,8 @@
 // lodestar_amd/js/signing_roots.js (getBlockSignatureSets for the TS host, SURVEY.md §8(f) row 2).
 //   node tests/js/test_signing_roots.js cpu [ops.json]  -> K3 devnet roots with a hashlib-style
 //        merkleizer (Node crypto); with ops.json, prints the roots of that block for the Python test
+//   node tests/js/test_signing_roots.js forks cases.json [gpu]  -> the fork / sync-participation /
+//        attester-slashing cases of tests/test_signing_roots.py fork_cases, roots or errors
 //   node tests/js/test_signing_roots.js gpu [ops.json]  -> the same through addon.merkleize (one
 //        launch per tree level), plus timings: the K3 block, a synthetic 128-attestation block, and a
 //        32-block range-sync segment (the reference's set construction takes ~45 ms per 100-signature
@@ -86,6 +88,32 @@ function opsRoots(file, merkleize) {
     keys: (s.type === "single" ? [s.pubkey] : s.pubkeys).map(hex)}));
 }
 
+/** fork cases written by tests/test_signing_roots.py (fork_cases): roots or the thrown error */
+function forkCaseRoots(file, merkleize) {
+  const cases = JSON.parse(fs.readFileSync(file, "utf8"));
+  const mainnet = {
+    genesisValidatorsRoot: hexb(cases.mainnet_gvr), forkPreviousVersion: new Uint8Array(4), forkCurrentVersion: new Uint8Array(4),
+    forkEpoch: 0, pubkey: (i) => Uint8Array.from(Buffer.from(i.toString(16).padStart(8, "0"), "hex")),
+    beaconCommittee: () => Array.from({length: 2048}, (_, k) => k),
+    syncCommittee: () => Array.from({length: 512}, (_, k) => k),
+    forkSeq: SR.forkSchedule(SR.MAINNET_FORK_EPOCHS),
+  };
+  return cases.cases.map((c) => {
+    let st = mainnet;
+    if (c.state === "k3") {
+      st = stateView(k3);
+      if (c.forks) st.forkSeq = SR.forkSchedule(c.forks);
+    }
+    try {
+      const sets = SR.resolve(SR.getBlockSignatureSets(st, c.block), merkleize);
+      return {case: c.name, sets: sets.map((s) => ({name: s.name, root: hex(s.signingRoot),
+        keys: (s.type === "single" ? [s.pubkey] : s.pubkeys).map(hex)}))};
+    } catch (e) {
+      return {case: c.name, error: e.message};
+    }
+  });
+}
+
 function time(fn, reps) {
   const ts = [];
   for (let r = 0; r < reps; r++) {
@@ -99,7 +127,19 @@ function time(fn, reps) {
 
 const mode = process.argv[2];
 const ops = process.argv[3];
-if (mode === "cpu") {
+if (mode === "forks") {
+  // node tests/js/test_signing_roots.js forks cases.json [gpu]
+  let m = cpuMerkleize;
+  let eng = null;
+  const addon = process.argv[4] === "gpu" ? require(path.join(__dirname, "..", "..", "lodestar_amd", "napi", "lodestar_bls.node")) : null;
+  if (addon) {
+    eng = addon.createEngine(0);
+    m = SR.gpuMerkleizer(eng);
+  }
+  console.log(JSON.stringify(forkCaseRoots(ops, m)));
+  if (addon) addon.destroyEngine(eng);
+  console.log("js fork cases ok");
+} else if (mode === "cpu") {
   checkK3(cpuMerkleize);
   if (ops) console.log(JSON.stringify(opsRoots(ops, cpuMerkleize)));
   console.log("js signing roots cpu ok");

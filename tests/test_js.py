@@ -137,3 +137,44 @@ def test_js_signing_roots_gpu(tmp_path):
     out = json.loads(lines[-2])
     assert out["ops"] == _python_ops_roots(ops)
     print("signing-root timings:", {k: v for k, v in out.items() if k != "ops"})
+
+
+def _fork_cases_file(tmp_path):
+    import json
+    from conftest import load_json
+    from test_signing_roots import MAINNET_GVR, fork_cases
+    cases = [{"name": n, "block": b, "state": kind, "forks": (None if forks in (None, "mainnet") else forks),
+              "err": err} for n, b, kind, forks, err in fork_cases(load_json("k3_devnet.json"))]
+    p = tmp_path / "fork_cases.json"
+    p.write_text(json.dumps({"mainnet_gvr": MAINNET_GVR, "cases": cases}))
+    return str(p)
+
+
+def _js_fork_cases(tmp_path, gpu):
+    import json
+    r = subprocess.run([NODE, SR_SCRIPT, "forks", _fork_cases_file(tmp_path)] + (["gpu"] if gpu else []),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[-1] == "js fork cases ok"
+    return json.loads(lines[-2])
+
+
+def test_js_fork_cases_cpu(tmp_path):
+    """the JS walk's fork dispatch (phase0 backfill blocks, altair, bellatrix), empty sync
+    participation (infinity: no set; otherwise the reference's error) and attester slashings equal
+    the Python walk's, which tests/test_signing_roots.py checks against oracle/ssz.py"""
+    if NODE is None:
+        pytest.skip("node not installed")
+    from conftest import load_json
+    from test_signing_roots import cpu_merkleize, python_fork_case_roots
+    assert _js_fork_cases(tmp_path, False) == python_fork_case_roots(load_json("k3_devnet.json"), cpu_merkleize)
+
+
+@pytest.mark.gpu
+def test_js_fork_cases_gpu(tmp_path):
+    if NODE is None:
+        pytest.skip("node not installed")
+    from conftest import load_json
+    from test_signing_roots import cpu_merkleize, python_fork_case_roots
+    assert _js_fork_cases(tmp_path, True) == python_fork_case_roots(load_json("k3_devnet.json"), cpu_merkleize)
