@@ -20,6 +20,9 @@ Secondary measurements on the same line (rank 0; N = 1 unless noted):
   value_one_batch_in_flight     one engine, the same batch
   value_distinct_roots          every signing root distinct (the no-sharing bound)
   value_one_invalid_per_batch   one wrong-message attestation per slot (the invalid-set search)
+  value_distinct_keys           the headline batches over a mainnet-sized resident table (2^20
+                                keys, ~10^6 validators as index2pubkey, pubkeyCache.ts:56-77):
+                                every validator id its own key, so the G1 gathers miss the cache
   value_e2e                     the headline batches through lb_verify_jobs_indexed with the same
                                 engines in flight: inputs in pinned host memory, so the pinned
                                 upload (H2D), the host-side chunk decomposition, every kernel and
@@ -79,7 +82,7 @@ def parse():
                     help="skip the secondary measurement with every signing root distinct (c3_distinct)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (invalid-set, slots1, latencies, per-config, drop-in)")
-    ap.add_argument("--legs", default="e2e,invalid,slots1,latency,configs,dropin,roots",
+    ap.add_argument("--legs", default="e2e,keys,invalid,slots1,latency,configs,dropin,roots",
                     help="secondary legs to run (comma list; A/B runs pick one)")
     ap.add_argument("--dropin-engines", type=int, default=4)
     ap.add_argument("--dropin-rounds", type=int, default=10, help="drop-in leg: timed rounds (median reported)")
@@ -301,6 +304,8 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     legs = set(a.legs.split(","))
     if wl_main is not None and "e2e" in legs:
         out.update(e2e_leg(a, engs, barrier, W, wl_main))
+    if "keys" in legs:
+        out.update(distinct_keys_leg(a, engs, barrier, W))
     if "invalid" in legs:
         out.update(invalid_leg(a, engs, barrier, W))
     wc1 = W.make(eng, "c1")
@@ -311,6 +316,36 @@ def extra_legs(a, engs, barrier, W, wl_main=None):
     if "configs" in legs:
         out["per_config"] = configs_leg(a, eng, W)
     return out, wc1
+
+
+def distinct_keys_leg(a, engs, barrier, W):
+    """value_distinct_keys: the c3 batch shape with validator v -> key v of a 2^20-key resident
+    table (SURVEY.md §8(d)'s distinct-key variant of the v mod 100 convention), batches in flight"""
+    t0 = time.time()
+    kp = W.KeyPool(engs[0], W.N_KEYS_MAINNET)
+    wk = W.make(engs[0], "c3", keys=kp, slots=a.slots) if a.slots > 1 else W.make(engs[0], "c3", keys=kp)
+    batches = [e.upload(W.indexed_for(e, wk)) for e in engs]
+    setup_s = time.time() - t0
+    assert np.array_equal(np.asarray(batches[0].verify()), wk.expected), "distinct-key verdicts differ"
+    steps = max(2, a.steps // 2)
+    el = run_inflight(batches, steps, wk.expected, barrier) if len(engs) > 1 else None
+    if el is None:
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            batches[0].verify()
+        barrier()
+        el = time.perf_counter() - t1
+    eng = engs[0]
+    prof = profiled_stages(eng, batches[0].verify)
+    for b in batches:
+        b.free()
+    idx = wk.packed.pk_indices
+    return {"value_distinct_keys": round(wk.packed.n_sets * steps * len(engs) / el, 1),
+            "distinct_keys": {"table_keys": len(kp.sks), "table_mb_per_engine": round(len(kp.sks) * 128 / 2 ** 20, 1),
+                              "key_gathers_per_batch": int(idx.size),
+                              "distinct_keys_per_batch": int(np.unique(idx).size),
+                              "pk_chunks_ms_one_batch": prof.get("pk_chunks"), "setup_s": round(setup_s, 1)}}
 
 
 def invalid_leg(a, engs, barrier, W):
@@ -509,7 +544,7 @@ def main():
 
         def xstep():
             # 576-byte partials over RCCL, one final exponentiation of their product (distributed.py)
-            codes, _ = verify_sharded(b.partial, e.product_is_one, b.verify, group=groups[k],
+            codes, _ = verify_sharded(b.partial, e.product_is_one, b.search_after_partial, group=groups[k],
                                       device=coll_dev if coll_dev.type == "cuda" else None)
             return codes
         return xstep

@@ -114,11 +114,17 @@ int32_t lb_batch_verify(lb_engine* e, lb_batch* b, const uint64_t* scalars, int3
  * and per-job error codes (out_job: -code for rejecting jobs, 1 otherwise).
  * lb_fp12_product_is_one multiplies n such partials and runs one final exponentiation;
  * *ok = 1 iff the product is 1 in GT (every valid job of every partial verifies).
- * On a 0 verdict, call lb_batch_verify on each shard to localise the invalid jobs.
+ * On a 0 verdict, lb_batch_search_after_partial localises each shard's invalid jobs from the
+ * state its lb_batch_partial left in the engine (the shard's own final exponentiation, then the
+ * invalid-set search, with the same blinding): no second pipeline run.  It returns
+ * LB_ERR_ARGUMENT if any other call ran on the engine in between (then call lb_batch_verify).
+ * Replaces the reference's per-job re-verification of a failing chunk
+ * (packages/beacon-node/src/chain/bls/multithread/worker.ts:76-98) for a sharded segment.
  */
 int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint8_t* out576,
                          int32_t* out_job);
 int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials576, uint32_t n, int32_t* ok);
+int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int32_t* out_job);
 
 /*
  * Upload + verify in one call (the worker's verifyManySignatureSets, worker.ts:32-108): inputs go

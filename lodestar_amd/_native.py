@@ -52,6 +52,7 @@ SIGNATURES = {
     "lb_batch_num_jobs": (ctypes.c_uint32, [_vp]),
     "lb_batch_verify": (ctypes.c_int32, [_vp, _vp, _u64p, _i32p]),
     "lb_batch_partial": (ctypes.c_int32, [_vp, _vp, _u64p, _u8p, _i32p]),
+    "lb_batch_search_after_partial": (ctypes.c_int32, [_vp, _vp, _i32p]),
     "lb_fp12_product_is_one": (ctypes.c_int32, [_vp, _u8p, ctypes.c_uint32, _i32p]),
     "lb_verify_jobs": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u32p, _u8p, _u8p, _u8p, _u32p, _u64p,
                                         _i32p]),

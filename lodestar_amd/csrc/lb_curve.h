@@ -168,6 +168,22 @@ LB_NI bool jac_to_aff(aff<F>& out, jac<F> p) {
   return !jac_is_inf(p);
 }
 
+// Register-only affine conversions for lone-lane stages of the wave kernels (jac_to_aff takes its
+// point by value through the stack: a private segment of ~0.7 KB per lane in kernels that run one
+// such conversion on one lane).  The only call is the product; the inversion is the inline EEA.
+LB_HD void g1_to_aff_inl(g1a& out, const g1j& p) {
+  const fp zi = fp_inv_i(p.z), zi2 = fp_sqr(zi);
+  out.x = fp_mul(p.x, zi2);
+  out.y = fp_mul(fp_mul(p.y, zi2), zi);
+}
+LB_HD void g2_to_aff_inl(g2a& out, const g2j& p) {
+  const fp ni = fp_inv_i(fp_add(fp_sqr(p.z.c0), fp_sqr(p.z.c1)));  // 1/z = conj(z) / N(z)
+  const fp2 zi{fp_mul(p.z.c0, ni), fp_neg(fp_mul(p.z.c1, ni))};
+  const fp2 zi2 = fp2_sqr(zi);
+  out.x = fp2_mul(p.x, zi2);
+  out.y = fp2_mul(fp2_mul(p.y, zi2), zi);
+}
+
 // [k]P for a 64-bit scalar, P affine (left-to-right double-and-add)
 template <class F>
 LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
@@ -352,6 +368,38 @@ LB_HD void g2_add_aff_lean(g2j& p, const g2a& q) {
   fp2 YJ = fp2_dbl(lean2_mul<kInl>(p.y, J));                             // Y dead
   p.x = fp2_sub(fp2_sub(lean2_sqr<kInl>(rr), J), fp2_dbl(V));           // J dead
   p.y = fp2_sub(lean2_mul<kInl>(rr, fp2_sub(V, p.x)), YJ);
+}
+
+// p + q for Jacobian p, q (add-2007-bl with the exceptional cases, as jac_add_i), register-lean
+// statement order for the lone-lane per-root kernels
+template <bool kInl>
+LB_HD void g2_add_lean(g2j& p, const g2j& q) {
+  if (jac_is_inf(q)) return;
+  if (jac_is_inf(p)) {
+    p = q;
+    return;
+  }
+  const fp2 Z1Z1 = lean2_sqr<kInl>(p.z), Z2Z2 = lean2_sqr<kInl>(q.z);
+  const fp2 ZZ = fp2_sub(fp2_sub(lean2_sqr<kInl>(fp2_add(p.z, q.z)), Z1Z1), Z2Z2);  // 2 Z1 Z2
+  const fp2 U1 = lean2_mul<kInl>(p.x, Z2Z2);
+  const fp2 S1 = lean2_mul<kInl>(lean2_mul<kInl>(p.y, q.z), Z2Z2);
+  const fp2 H = fp2_sub(lean2_mul<kInl>(q.x, Z1Z1), U1);
+  const fp2 rr = fp2_dbl(fp2_sub(lean2_mul<kInl>(lean2_mul<kInl>(q.y, p.z), Z1Z1), S1));
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(rr)) {
+      p = q;
+      g2_dbl_lean<kInl>(p);
+    } else {
+      p = jac_infinity<fp2>();
+    }
+    return;
+  }
+  p.z = lean2_mul<kInl>(ZZ, H);
+  const fp2 I = lean2_sqr<kInl>(fp2_dbl(H));
+  const fp2 J = lean2_mul<kInl>(H, I);
+  const fp2 V = lean2_mul<kInl>(U1, I);
+  p.x = fp2_sub(fp2_sub(lean2_sqr<kInl>(rr), J), fp2_dbl(V));
+  p.y = fp2_sub(lean2_mul<kInl>(rr, fp2_sub(V, p.x)), fp2_dbl(lean2_mul<kInl>(S1, J)));
 }
 
 // The loop is kept rolled, and the base point is re-read from memory (`src`, the caller's

@@ -113,7 +113,16 @@ struct lb_engine {
   dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
       set_live, gacc, gp_aff, gp_inf;
   // bucket MSM for sum r_i sig_i (k_msm_*)
-  dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum;
+  dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
+  // k_hash_finish's parked points (4 x 72 words per launched lane)
+  dbuf park;
+  // the batch whose lb_batch_partial left its state (trees, statuses, scalars) in this engine's
+  // workspace, for lb_batch_search_after_partial; any other pipeline run clears it
+  lb_batch* partial_batch = nullptr;
+  uint32_t partial_mu = 0;
+  // bucket sums and the bucket reduction by 8-lane groups (k_msm_buckets_g8, k_msm_window_g8,
+  // k_msm_horner_g8); LB_MSM_G8=0: the lone-lane kernels (k_msm_buckets, k_msm_reduce)
+  bool msm_g8 = true;
   // invalid-set search (search_invalid): node descriptors and per-node results
   dbuf sx[32];   // search round buffers (search_invalid: SX_*)
   dbuf pk_aff;  // affine aggregate pubkey per set (single-set checks of the search)
@@ -151,8 +160,8 @@ struct lb_engine {
   // search's first-round subtrees hold comparable numbers of sets (LB_ROOT_SHUFFLE=0: input order)
   bool root_shuffle = true;
   std::vector<uint64_t> h_scalars;
-  // resident pubkey table: g1a SoA (24 words x table_cap) + per-entry flag
-  dbuf table, table_flag;
+  // resident pubkey table: one 128-byte record per key (g1a + flag, LB_TABLE_REC words)
+  dbuf table;
   uint32_t table_n = 0, table_cap = 0;
   // KZG trusted setup (lb_kzg_load_setup): [tau^i] G1 as g1a SoA (kzg_n entries), [tau^0,1] G2
   dbuf kzg_g1, kzg_g2;
@@ -296,6 +305,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
@@ -317,29 +327,6 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
   }
-  // Size s1's scratch now, one engine at a time, for the one-lane per-root kernels with large
-  // private segments (k_miller_lane, k_hash_finish): an empty dispatch over more waves than the
-  // device holds.  Several queues growing their scratch at the same moment (batches in flight
-  // switching to the one-lane form together) abort with HSA_STATUS_ERROR_OUT_OF_RESOURCES.
-  // (Not when the one-lane Miller form is disabled, LB_MILLER_FORM=g8: the queue then never needs
-  // that private segment, and every queue's scratch counts against one per-process pool.)
-  if (e->miller_form != 2) {
-    // the lock covers only the dispatch: lb_engine_destroy takes it again on the error path
-    bool ok;
-    {
-      std::lock_guard<std::mutex> lk(g_engine_mu);
-      ok = e->n_u.ensure(4) == hipSuccess && hipMemsetAsync(e->n_u.p, 0, 4, e->stream) == hipSuccess;
-      if (ok) {
-        hipLaunchKernelGGL(k_miller_lane, dim3(4096), dim3(LB_TPB), 0, e->stream, 0u, 1u, e->n_u.as<uint32_t>(),
-                           nullptr, nullptr, nullptr, nullptr);
-        ok = hipStreamSynchronize(e->stream) == hipSuccess;
-      }
-    }
-    if (!ok) {
-      lb_engine_destroy(e);
-      return LB_ERR_DEVICE;
-    }
-  }
   *out = e;
   return LB_OK;
 }
@@ -350,11 +337,11 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamSynchronize(e->stream);
   dbuf* bufs[] = {&e->scalars, &e->sig_aff, &e->sig_inf, &e->sig_status, &e->q, &e->h_aff, &e->rpk, &e->rsig,
                   &e->pk_status, &e->ml, &e->treeP, &e->treeS, &e->job_status, &e->nodes, &e->verdict, &e->parts,
-                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->table_flag, &e->msg_tab,
+                  &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->msg_tab,
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
-                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->pk_aff, &e->y_root, &e->kzg_g1,
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->wsum, &e->park, &e->pk_aff, &e->y_root, &e->kzg_g1,
                   &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
@@ -528,23 +515,16 @@ int32_t lb_pubkey_table_append(lb_engine* e, uint32_t n, const uint8_t* keys, ui
   if (!n) return LB_OK;
   const uint32_t need = first + n;
   if (need > e->table_cap) {
-    // grow: SoA stride changes, so move word rows one by one
+    // grow: records keep their layout, one contiguous copy
     uint32_t cap = e->table_cap ? e->table_cap : 1024;
     while (cap < need) cap *= 2;
-    dbuf nt, nf;
-    LB_HIP(nt.ensure((size_t)cap * sizeof(g1a)));
-    LB_HIP(nf.ensure((size_t)cap * 4));
-    const int words = (int)(sizeof(g1a) / 4);
-    for (int w = 0; w < words && first; w++)
-      LB_HIP(hipMemcpyAsync(nt.as<uint32_t>() + (size_t)w * cap, e->table.as<uint32_t>() + (size_t)w * e->table_cap,
-                            (size_t)first * 4, hipMemcpyDeviceToDevice, e->stream));
+    dbuf nt;
+    LB_HIP(nt.ensure((size_t)cap * LB_TABLE_REC * 4));
     if (first)
-      LB_HIP(hipMemcpyAsync(nf.p, e->table_flag.p, (size_t)first * 4, hipMemcpyDeviceToDevice, e->stream));
+      LB_HIP(hipMemcpyAsync(nt.p, e->table.p, (size_t)first * LB_TABLE_REC * 4, hipMemcpyDeviceToDevice, e->stream));
     LB_HIP(hipStreamSynchronize(e->stream));
     e->table.release();
-    e->table_flag.release();
     e->table = nt;
-    e->table_flag = nf;
     e->table_cap = cap;
   }
   dbuf kin, st;
@@ -553,8 +533,7 @@ int32_t lb_pubkey_table_append(lb_engine* e, uint32_t n, const uint8_t* keys, ui
   if (r == hipSuccess) r = hipMemcpyAsync(kin.p, keys, (size_t)n * key_size, hipMemcpyHostToDevice, e->stream);
   if (r == hipSuccess) {
     hipLaunchKernelGGL(k_table_fill, dim3(nblk(n)), dim3(LB_TPB), 0, e->stream, n, kin.as<uint8_t>(), key_size,
-                       validate, first, e->table.as<uint32_t>(), e->table_cap, e->table_flag.as<uint32_t>(),
-                       st.as<int32_t>());
+                       validate, first, e->table.as<uint32_t>(), st.as<int32_t>());
     r = hipGetLastError();
   }
   if (r == hipSuccess) r = hipMemcpyAsync(out_status, st.p, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream);
@@ -595,11 +574,42 @@ struct stage_scope {
   }
 };
 
+// Bucket sums -> S_j = sum_d d B_d per instance j (n_inst instances of W windows, buckets
+// [j W 256, (j+1) W 256) of bsum) -> element out0 + j of `out` (SoA, stride n_out).
+static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32_t nb, uint32_t n_inst, int W,
+                             uint32_t* out, uint32_t n_out, uint32_t out0) {
+  if (e->msm_g8) {
+    hipError_t r = e->wsum.ensure((size_t)n_inst * W * sizeof(g2j));
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(), bcap,
+                       e->bsum.as<uint32_t>(), nb);
+    hipLaunchKernelGGL(k_msm_window_g8, dim3(n_inst * W), dim3(256), 0, st, e->bsum.as<uint32_t>(), nb,
+                       e->wsum.as<uint32_t>(), n_inst * W);
+    if (W == LB_MSM_W)
+      hipLaunchKernelGGL(k_msm_horner_g8<LB_MSM_W>, dim3((n_inst + 7) / 8), dim3(64), 0, st, e->wsum.as<uint32_t>(),
+                         n_inst, out, n_out, out0);
+    else
+      hipLaunchKernelGGL(k_msm_horner_g8<LB_SMSM_W>, dim3((n_inst + 7) / 8), dim3(64), 0, st, e->wsum.as<uint32_t>(),
+                         n_inst, out, n_out, out0);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(),
+                     bcap, e->bsum.as<uint32_t>(), nb);
+  if (W == LB_MSM_W)
+    hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(n_inst), dim3(64 * LB_MSM_W), 0, st, e->bsum.as<uint32_t>(), nb, out,
+                       n_out, out0);
+  else
+    hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(n_inst), dim3(64 * LB_SMSM_W), 0, st, e->bsum.as<uint32_t>(), nb,
+                       out, n_out, out0);
+  return hipGetLastError();
+}
+
 // Runs the batch pipeline on two streams: the job S tree (leaf count mj = pow2 >= jobs) with
 // fS = ML(-G1, S_root) on s2, the message product tree (leaf count mu = pow2 >= sets, leaves
 // [0, n_u) live) on s1, joined on s1 ready for the root check.
 static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
+  e->partial_batch = nullptr;
   int st = fill_scalars(e, n, scalars);
   if (st != LB_OK) return st;
   mj = 1;
@@ -672,8 +682,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       stage_scope sc(e, ST_PK_CHUNKS, s3);
       if (nc && b->indexed)
         hipLaunchKernelGGL(k_pk_chunks_idx, dim3(nblk(nc)), dim3(LB_TPB), 0, s3, nc, b->d_chunk_lo.as<uint32_t>(),
-                           b->d_pks.as<uint32_t>(), e->table.as<uint32_t>(), e->table_cap,
-                           e->table_flag.as<uint32_t>(), e->table_n, e->chunk_acc.as<uint32_t>(),
+                           b->d_pks.as<uint32_t>(), e->table.as<uint32_t>(), e->table_n, e->chunk_acc.as<uint32_t>(),
                            e->chunk_status.as<int32_t>());
       else if (nc)
         hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s3, nc, b->d_chunk_lo.as<uint32_t>(),
@@ -751,8 +760,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
                            e->h_aff.as<uint32_t>());
       else
+      {
+        const uint32_t pn = nblk_inv(nuh) * LB_INV_TPB;  // one park column per launched lane
+        LB_HIP(e->park.ensure((size_t)4 * 72 * 4 * (pn > n ? pn : n)));
         hipLaunchKernelGGL(k_hash_finish, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->q.as<uint32_t>(),
-                           e->h_aff.as<uint32_t>());
+                           e->h_aff.as<uint32_t>(), e->park.as<uint32_t>(), pn);
+      }
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
     if (n <= e->small_s_max) {
@@ -793,10 +806,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
-      hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(LB_MSM_NB)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
-                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB);
-      hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(1), dim3(64 * LB_MSM_W), 0, s2, e->bsum.as<uint32_t>(), (uint32_t)LB_MSM_NB,
-                         e->treeS.as<uint32_t>(), 2 * mj, 1u);
+      LB_HIP(msm_reduce(e, s2, bcap, LB_MSM_NB, 1u, LB_MSM_W, e->treeS.as<uint32_t>(), 2 * mj, 1u));
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
     LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
@@ -1130,14 +1140,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
-      hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
-                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
-      if (w4)
-        hipLaunchKernelGGL(k_msm_reduce<LB_MSM_W>, dim3(cm), dim3(64 * LB_MSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
-                           U(SX_S), cm, 0u);
-      else
-        hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(cm), dim3(64 * LB_SMSM_W), 0, s1, e->bsum.as<uint32_t>(), nb,
-                           U(SX_S), cm, 0u);
+      LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u));
     }
     if (c)
       hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),
@@ -1493,7 +1496,39 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   LB_HIP(hipStreamSynchronize(e->stream));
   for (uint32_t j = 0; j < b->n_jobs; j++) out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
   finish_profile(e);
+  e->partial_batch = b;
+  e->partial_mu = mu;
   return LB_OK;
+}
+
+extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int32_t* out_job) {
+  if (!e || !b || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (b->n_jobs == 0) return LB_OK;
+  if (e->partial_batch != b) return LB_ERR_ARGUMENT;  // another call ran on this engine since
+  LB_HIP(hipSetDevice(e->device));
+  busy_scope busy(e->device);
+  const uint32_t mu = e->partial_mu, nj = b->n_jobs;
+  LB_HIP(e->verdict.ensure(4));
+  LB_HIP(e->y_root.ensure(576));
+  // this shard's own root check: a passing shard is done, a failing one searches from it
+  hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(), e->fS.as<uint32_t>(),
+                     e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
+  LB_HIP(hipGetLastError());
+  std::vector<int32_t> jst(nj);
+  int32_t root_ok = 0;
+  LB_HIP(hipMemcpyAsync(jst.data(), e->job_status.p, (size_t)nj * 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipMemcpyAsync(&root_ok, e->verdict.p, 4, hipMemcpyDeviceToHost, e->stream));
+  LB_HIP(hipStreamSynchronize(e->stream));
+  bool any_live = false;
+  for (uint32_t j = 0; j < nj; j++) {
+    out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
+    any_live |= jst[j] == LB_OK;
+  }
+  int32_t st = LB_OK;
+  if (any_live && !root_ok) st = search_invalid(e, b, mu, out_job);
+  e->partial_batch = nullptr;
+  return st;
 }
 
 extern "C" int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials576, uint32_t n, int32_t* ok) {

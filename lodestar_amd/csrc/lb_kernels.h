@@ -291,37 +291,152 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32
   soa_st(q, 2 * n, which * n + u, p);
 }
 
-// block of LB_INV_TPB threads (fp_inv_block)
-__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_hash_finish(uint32_t n, const uint32_t* __restrict__ n_u,
-                                                            const uint32_t* __restrict__ q,
-                                                            uint32_t* __restrict__ h_aff) {
+// Lone-lane state parked in an engine-owned global buffer (word w of slot k of root u at
+// st[(k * 72 + w) * n + u]: a wave's lanes touch consecutive words), so long-lived points do not
+// stay in registers across a 63-step ladder.  The memory clobber ends the register copy's life:
+// later uses reload.  The runtime's private segment (scratch) is reserved per HIP queue for the
+// device's whole wave capacity, so kilobytes of spill per lane in any kernel cap the engines per
+// device; this buffer is sized by the launch.
+__device__ __forceinline__ void lane_park(uint32_t* __restrict__ st, uint32_t n, uint32_t u, int k, const g2j& p) {
+  soa_st(st + (size_t)k * 72 * n, n, u, p);
+  __asm__ volatile("" ::: "memory");
+}
+__device__ __forceinline__ g2j lane_unpark(const uint32_t* __restrict__ st, uint32_t n, uint32_t u, int k) {
+  __asm__ volatile("" ::: "memory");
+  return soa_ld<g2j>(st + (size_t)k * 72 * n, n, u);
+}
+__device__ __forceinline__ void lane_park_aff(uint32_t* __restrict__ st, uint32_t n, uint32_t u, int k, const g2a& p) {
+  soa_st(st + (size_t)k * 72 * n, n, u, p);
+  __asm__ volatile("" ::: "memory");
+}
+__device__ __forceinline__ g2a lane_unpark_aff(const uint32_t* __restrict__ st, uint32_t n, uint32_t u, int k) {
+  __asm__ volatile("" ::: "memory");
+  return soa_ld<g2a>(st + (size_t)k * 72 * n, n, u);
+}
+// [|x|] (affine point in slot k; `inf`: the point at infinity, whose multiple is infinity): lean
+// inline doublings and mixed additions, the base re-read at the five additions
+__device__ __forceinline__ g2j g2_mul_xabs_parked(const uint32_t* st, uint32_t n, uint32_t u, int k, bool inf) {
+  if (inf) return jac_infinity<fp2>();
+  g2j acc = jac_from_aff(lane_unpark_aff(st, n, u, k));
+#pragma clang loop unroll(disable)
+  for (int i = 62; i >= 0; i--) {
+    g2_dbl_lean<true>(acc);
+    if ((LB_X_ABS >> i) & 1ull) {
+      if (jac_is_inf(acc))
+        acc = jac_from_aff(lane_unpark_aff(st, n, u, k));
+      else
+        g2_add_aff_lean<true>(acc, lane_unpark_aff(st, n, u, k));
+    }
+  }
+  return acc;
+}
+__device__ __forceinline__ void g2_add_aff_or(g2j& p, const g2a& q) {
+  if (jac_is_inf(p))
+    p = jac_from_aff(q);
+  else
+    g2_add_aff_lean<true>(p, q);
+}
+__device__ __forceinline__ g2a g2_psi_aff(const g2a& a) {
+  return g2a{fp2_mul(fp2_conj(a.x), fp2_load(LB_PSI_CX)), fp2_mul(fp2_conj(a.y), fp2_load(LB_PSI_CY))};
+}
+__device__ __forceinline__ g2a g2a_neg(const g2a& a) { return g2a{a.x, fp2_neg(a.y)}; }
+// Jacobian -> affine for every lane of the block (fp_inv_block: one inversion per block); inf
+// reports the point at infinity (its affine value is then meaningless)
+__device__ __forceinline__ g2a g2_to_aff_block(const g2j& h, bool act, bool& inf) {
+  const fp nz = fp_add(fp_sqr(h.z.c0), fp_sqr(h.z.c1));
+  inf = !act || fp_is_zero(nz);
+  const fp ni = fp_inv_block<true>(inf ? fp_one() : nz);  // inline EEA: no by-value call frames
+  const fp2 zi{fp_mul(h.z.c0, ni), fp_neg(fp_mul(h.z.c1, ni))};
+  const fp2 zi2 = fp2_sqr(zi);
+  return g2a{fp2_mul(h.x, zi2), fp2_mul(fp2_mul(h.y, zi2), zi)};
+}
+
+// p + q for Jacobian p and a PARKED Jacobian q (slot k, negated if neg): q's coordinates are
+// read when each is needed, so p, q and the formula's temporaries are never live together
+// (add-2007-bl with Z1 Z2 by one product; the exceptional cases as g2_add_lean)
+__device__ __forceinline__ void g2_add_parked(g2j& p, const uint32_t* st, uint32_t n, uint32_t u, int k, bool neg) {
+  const uint32_t* b = st + (size_t)k * 72 * n;
+  auto ld2 = [&](int c) {  // coordinate c of q
+    __asm__ volatile("" ::: "memory");
+    return soa_ld<fp2>(b + (size_t)24 * c * n, n, u);
+  };
+  const fp2 qz = ld2(2);
+  if (fp2_is_zero(qz)) return;  // q = infinity
+  if (jac_is_inf(p)) {
+    p = lane_unpark(st, n, u, k);
+    if (neg) p = jac_neg(p);
+    return;
+  }
+  const fp2 Z2Z2 = lean2_sqr<true>(qz);
+  const fp2 Z1Z2 = lean2_mul<true>(p.z, qz);
+  const fp2 U1 = lean2_mul<true>(p.x, Z2Z2);
+  const fp2 S1 = lean2_mul<true>(lean2_mul<true>(p.y, qz), Z2Z2);
+  const fp2 Z1Z1 = lean2_sqr<true>(p.z);
+  const fp2 H = fp2_sub(lean2_mul<true>(ld2(0), Z1Z1), U1);
+  fp2 S2 = lean2_mul<true>(lean2_mul<true>(ld2(1), p.z), Z1Z1);
+  if (neg) S2 = fp2_neg(S2);
+  const fp2 rr = fp2_dbl(fp2_sub(S2, S1));
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(rr)) {
+      p = lane_unpark(st, n, u, k);
+      if (neg) p = jac_neg(p);
+      g2_dbl_lean<true>(p);
+    } else {
+      p = jac_infinity<fp2>();
+    }
+    return;
+  }
+  p.z = fp2_dbl(lean2_mul<true>(Z1Z2, H));
+  const fp2 I = lean2_sqr<true>(fp2_dbl(H));
+  const fp2 J = lean2_mul<true>(H, I);
+  const fp2 V = lean2_mul<true>(U1, I);
+  p.x = fp2_sub(fp2_sub(lean2_sqr<true>(rr), J), fp2_dbl(V));
+  p.y = fp2_sub(lean2_mul<true>(rr, fp2_sub(V, p.x)), fp2_dbl(lean2_mul<true>(S1, J)));
+}
+
+// block of LB_INV_TPB threads (fp_inv_block).  h_eff Q via psi (as g2_clear_cofactor) with the
+// two [x] ladders over AFFINE bases (the block's batch inversions make them affine: mixed
+// additions, 5 x 14 fewer products per ladder and a smaller live set) and the long-lived points
+// parked (slots: 0 Q, 1 t1 = [x]Q, 2 t3, 3 t1 + psi(Q); 4 x 72 words per lane, stride pn >= grid).
+__global__ void __launch_bounds__(LB_INV_TPB, 1) k_hash_finish(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                                  const uint32_t* __restrict__ q,
+                                                                  uint32_t* __restrict__ h_aff,
+                                                                  uint32_t* __restrict__ park, uint32_t pn) {
   const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
   const uint32_t nu = *n_u;
   if (blockIdx.x * LB_INV_TPB >= nu) return;  // whole block idle (uniform: fp_inv_block is safe)
   const bool act = i < nu;
-  g2j h = jac_infinity<fp2>();
-  if (act) {
-    g2j q0 = soa_ld<g2j>(q, 2 * n, i);
-    g2j q1 = soa_ld<g2j>(q, 2 * n, n + i);
-    h = g2_clear_cofactor(jac_add(q0, q1));
+  const uint32_t ic = act ? i : nu - 1;  // idle lanes compute a live root's values, store nothing
+  // (each lane parks in its own column i < pn)
+  bool inf0, inf1, inf2;
+  {
+    g2j h = soa_ld<g2j>(q, 2 * n, ic);
+    g2_add_parked(h, q, 2 * n, n + ic, 0, false);  // Q = Q0 + Q1 (Q1: element n + ic of q, "slot 0")
+    lane_park_aff(park, pn, i, 0, g2_to_aff_block(h, act, inf0));
   }
-  // 1/z = conj(z) / N(z): batch-invert the norm.  H(m) == infinity has negligible probability;
-  // its z = 0 gives x = y = 0 as jac_to_aff would.
-  const fp nz = fp_add(fp_sqr(h.z.c0), fp_sqr(h.z.c1));
-  const bool zero = fp_is_zero(nz);
-  const fp ni = fp_inv_block(zero ? fp_one() : nz);
-  if (!act) return;
-  g2a a;
-  if (zero) {
-    a.x = fp2_zero();
-    a.y = fp2_zero();
+  lane_park(park, pn, i, 1, jac_neg(g2_mul_xabs_parked(park, pn, i, 0, inf0)));  // t1 = [x] Q
+  g2j b = lane_unpark(park, pn, i, 1);
+  if (!inf0) {
+    const g2a qa = lane_unpark_aff(park, pn, i, 0);
+    g2j t3 = jac_from_aff(qa);
+    g2_dbl_lean<true>(t3);
+    t3 = g2_psi2(t3);
+    g2_add_aff_or(t3, g2a_neg(g2_psi_aff(qa)));  // psi^2(2Q) - psi(Q)
+    lane_park(park, pn, i, 2, t3);
+    g2_add_aff_or(b, g2_psi_aff(qa));  // t1 + psi(Q)
   } else {
-    const fp2 zi{fp_mul(h.z.c0, ni), fp_neg(fp_mul(h.z.c1, ni))};
-    const fp2 zi2 = fp2_sqr(zi);
-    a.x = fp2_mul(h.x, zi2);
-    a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
+    lane_park(park, pn, i, 2, jac_infinity<fp2>());
   }
-  soa_st(h_aff, n, i, a);
+  lane_park_aff(park, pn, i, 3, g2_to_aff_block(b, act, inf1));
+  lane_park(park, pn, i, 3, jac_neg(g2_mul_xabs_parked(park, pn, i, 3, inf1)));  // t2x = [x](t1 + psi(Q))
+  g2j h = lane_unpark(park, pn, i, 2);
+  g2_add_parked(h, park, pn, i, 3, false);
+  g2_add_parked(h, park, pn, i, 1, true);
+  if (!inf0) g2_add_aff_or(h, g2a_neg(lane_unpark_aff(park, pn, i, 0)));
+  // H(m) == infinity has negligible probability; its z = 0 gives x = y = 0 as jac_to_aff would
+  const g2a a = g2_to_aff_block(h, act, inf2);
+  if (!act) return;
+  soa_st(h_aff, n, i, inf2 ? g2a{fp2_zero(), fp2_zero()} : a);
 }
 
 // The same with 8 lanes per root (lb_group.h: each G2 doubling in 3 levels of Fp products, each
@@ -381,12 +496,22 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, cons
   chunk_status[c] = st;
 }
 
-// Same as k_pk_chunks over the resident pubkey table (affine Montgomery, g1a SoA with
-// table_cap elements).  table_flag[t] = (decode status << 1) | is_infinity.  idx = pk_indices.
+// The resident pubkey table (the epoch cache's index2pubkey, pubkeyCache.ts:56-77): one 128-byte
+// record per key, words 0-23 the affine Montgomery point (g1a), word 24 the flag (decode status
+// << 1) | is_infinity.  A gather by validator index touches one L2 line (a word-major layout
+// touched 24 lines + 1 for the flag: with a mainnet-sized table every one a miss).
+#define LB_TABLE_REC 32
+__device__ __forceinline__ g1a table_ld(const uint32_t* __restrict__ table, uint32_t t) {
+  return aos_ld<g1a>(table + (size_t)LB_TABLE_REC * t, 0);
+}
+__device__ __forceinline__ uint32_t table_flag_ld(const uint32_t* __restrict__ table, uint32_t t) {
+  return table[(size_t)LB_TABLE_REC * t + 24];
+}
+
+// Same as k_pk_chunks over the resident pubkey table.  idx = pk_indices.
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                           const uint32_t* __restrict__ idx,
-                                                          const uint32_t* __restrict__ table, uint32_t table_cap,
-                                                          const uint32_t* __restrict__ table_flag, uint32_t table_n,
+                                                          const uint32_t* __restrict__ table, uint32_t table_n,
                                                           uint32_t* __restrict__ chunk_acc,
                                                           int32_t* __restrict__ chunk_status) {
   uint32_t c = lb_tid();
@@ -400,13 +525,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
       st = LB_ERR_ARGUMENT;
       break;
     }
-    const uint32_t fl = table_flag[t];
+    const uint32_t fl = table_flag_ld(table, t);
     if (fl >> 1) {
       st = (int)(fl >> 1);
       break;
     }
     if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
-    acc = jac_add_aff_i<lb_g1f, true>(acc, aff_as<lb_g1f>(soa_ld<g1a>(table, table_cap, t)));
+    acc = jac_add_aff_i<lb_g1f, true>(acc, aff_as<lb_g1f>(table_ld(table, t)));
   }
   soa_st(chunk_acc, nc, c, jac_as<fp>(acc));
   chunk_status[c] = st;
@@ -415,8 +540,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
 // decode keys into the resident table (48 B compressed or 96 B uncompressed)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, const uint8_t* __restrict__ keys,
                                                        uint32_t key_size, int32_t validate, uint32_t first,
-                                                       uint32_t* __restrict__ table, uint32_t table_cap,
-                                                       uint32_t* __restrict__ table_flag, int32_t* __restrict__ status) {
+                                                       uint32_t* __restrict__ table, int32_t* __restrict__ status) {
   uint32_t i = lb_tid();
   if (i >= n) return;
   g1a a;
@@ -444,8 +568,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
     a.x = fp_zero();
     a.y = fp_zero();
   }
-  soa_st(table, table_cap, first + i, a);
-  table_flag[first + i] = ((uint32_t)st << 1) | (inf ? 1u : 0u);
+  uint32_t* rec = table + (size_t)LB_TABLE_REC * (first + i);
+  aos_st(rec, 0, a);
+  uint4 tail = {((uint32_t)st << 1) | (inf ? 1u : 0u), 0u, 0u, 0u};
+  reinterpret_cast<uint4*>(rec)[6] = tail;
   status[i] = st;
 }
 
@@ -847,6 +973,114 @@ __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restric
   }
 }
 
+// ---- the same bucket reduction by 8-lane groups (lb_group.h), for the latency of the chain: a
+// G2 addition is 6 product levels on a group instead of 43 serial products on a lone lane.
+// Group point exchange through LDS (every lane of the group writes the same replicated words:
+// a lane-dependent word index would put the point on the stack).
+__device__ __forceinline__ void g8_put(lds_u32* X, int slot, const g2j& p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&p);
+  LB_UNROLL for (int k = 0; k < 72; k++) X[72 * slot + k] = w[k];
+}
+__device__ __forceinline__ g2j g8_take(const lds_u32* X, int slot) {
+  g2j p;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&p);
+  LB_UNROLL for (int k = 0; k < 72; k++) w[k] = X[72 * slot + k];
+  return p;
+}
+__device__ __forceinline__ g2j g2j_shfl(const g2j& a, int src) {
+  g2j r;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+  LB_UNROLL for (int k = 0; k < 72; k++) o[k] = __shfl(w[k], src, 64);
+  return r;
+}
+// bucket b = sum of its chunk sums: one wave per bucket, group g sums chunks g, g + 8, ..., then a
+// 3-level shuffle tree over the groups (as k_msm_buckets, whose lone lane summed ~60 chunk sums
+// serially)
+__global__ void __launch_bounds__(64) k_msm_buckets_g8(const uint32_t* __restrict__ bch,
+                                                       const uint32_t* __restrict__ bacc, uint32_t cap,
+                                                       uint32_t* __restrict__ bsum, uint32_t nb) {
+  const uint32_t b = blockIdx.x;
+  if (b >= nb) return;
+  const int g = threadIdx.x >> 3;
+  g2j acc = jac_infinity<fp2>();
+#pragma clang loop unroll(disable)
+  for (uint32_t c = bch[b] + g; c < bch[b + 1]; c += 8) g8_add(acc, soa_ld<g2j>(bacc, cap, c));
+#pragma clang loop unroll(disable)
+  for (int d = 4; d >= 1; d >>= 1) {
+    const g2j o = g2j_shfl(acc, ((int)threadIdx.x + 8 * d) & 63);
+    if (g < d) g8_add(acc, o);
+  }
+  if (threadIdx.x == 0) soa_st(bsum, nb, b, acc);
+}
+// Window sums W_w = sum_d d B_d of k_msm_reduce, one workgroup of 4 waves per (instance, window)
+// (one wave per SIMD: a group's G2 addition needs more than 256 registers): group s owns digits
+// [8 s, 8 s + 8) (Y_s = sum_j j B_{8s+j}, T_s = sum_j B_{8s+j}: 13 additions), a 5-level suffix
+// scan U_s = sum_{t >= s} T_t over the 32 groups, V_s = Y_s + 8 U_s (s >= 1), a 5-level tree:
+// sum_d d B_d = sum_s (Y_s + 8 s T_s) = sum_s Y_s + 8 sum_{k >= 1} U_k.
+// wsum: element blockIdx.x = instance * W + w.
+__global__ void __launch_bounds__(256) k_msm_window_g8(const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                       uint32_t* __restrict__ wsum, uint32_t n_w) {
+  static_assert(LB_MSM_B == 256, "32 groups of 8 digits per window");
+  __shared__ uint32_t xs[32 * 72], ys[32 * 72];
+  lds_u32* X = (lds_u32*)xs;
+  lds_u32* Y = (lds_u32*)ys;
+  const int s = threadIdx.x >> 3;
+  const uint32_t e0 = blockIdx.x * LB_MSM_B + 8 * s;  // bucket (instance, w, d) at instance*W*256 + w*256 + d
+  g2j run = soa_ld<g2j>(bsum, nb, e0 + 7);
+  g2j y = run;
+#pragma clang loop unroll(disable)
+  for (int j = 6; j >= 1; j--) {
+    g8_add(run, soa_ld<g2j>(bsum, nb, e0 + j));
+    g8_add(y, run);
+  }
+  if (s) g8_add(run, soa_ld<g2j>(bsum, nb, e0));  // digit 0 is unused
+  g8_put(Y, s, y);
+  // inclusive suffix scan: u_s = sum_{t >= s} T_t
+#pragma clang loop unroll(disable)
+  for (int d = 1; d < 32; d <<= 1) {
+    g8_put(X, s, run);
+    __syncthreads();
+    g2j o = jac_infinity<fp2>();
+    if (s + d < 32) o = g8_take(X, s + d);
+    __syncthreads();
+    if (s + d < 32) g8_add(run, o);
+  }
+  g2j v = g8_take(Y, s);
+  if (s) {
+    g8_dbl(run);
+    g8_dbl(run);
+    g8_dbl(run);
+    g8_add(v, run);
+  }
+#pragma clang loop unroll(disable)
+  for (int d = 16; d >= 1; d >>= 1) {
+    g8_put(X, s, v);
+    __syncthreads();
+    g2j o = jac_infinity<fp2>();
+    if (s < d) o = g8_take(X, s + d);
+    __syncthreads();
+    if (s < d) g8_add(v, o);
+  }
+  if (threadIdx.x == 0) soa_st(wsum, n_w, blockIdx.x, v);
+}
+// S_j = sum_w 2^(8 w) W_w (Horner) for instance j = 8 blockIdx.x + group -> out0 + j of `out`
+template <int W>
+__global__ void __launch_bounds__(64) k_msm_horner_g8(const uint32_t* __restrict__ wsum, uint32_t n_inst,
+                                                      uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
+  const uint32_t j = blockIdx.x * 8 + (threadIdx.x >> 3);
+  if (j >= n_inst) return;  // uniform within the group
+  const uint32_t n_w = n_inst * W;
+  g2j S = soa_ld<g2j>(wsum, n_w, j * W + W - 1);
+#pragma clang loop unroll(disable)
+  for (int ww = W - 2; ww >= 0; ww--) {
+#pragma clang loop unroll(disable)
+    for (int b = 0; b < LB_MSM_C; b++) g8_dbl(S);
+    g8_add(S, soa_ld<g2j>(wsum, n_w, j * W + ww));
+  }
+  if (g8_q() == 0) soa_st(out, n_out, out0 + j, S);
+}
+
 // Small batches: S = sum r_i sig_i without the bucket MSM, whose chunk / bucket / reduction
 // chain is a fixed ~5 ms of serial G2 additions however few the sets.  Each live set's r_i sig_i
 // by 8 lanes (k_sig_blind_g8: GLV double-and-add, [lambda] sig = -psi^2(sig)), then 64:1 shuffle
@@ -1183,7 +1417,7 @@ __device__ void w_miller_pk(fp* S, int dst, const g1j& pj_lane0, const uint32_t*
     s_inf = jac_is_inf(pj_lane0) ? 1 : 0;
     if (!s_inf) {
       g1a pa;
-      jac_to_aff(pa, pj_lane0);
+      g1_to_aff_inl(pa, pj_lane0);
       const g2a h = soa_ld<g2a>(h_aff, n, u);
       w_st(S, LBW_PT + 0, pa.x);
       w_st(S, LBW_PT + 1, pa.y);
@@ -1208,7 +1442,7 @@ __device__ void w_miller_negg1(fp* S, int dst, const g2j& q_lane0) {
     s_inf = jac_is_inf(q_lane0) ? 1 : 0;
     if (!s_inf) {
       g2a a;
-      jac_to_aff(a, q_lane0);
+      g2_to_aff_inl(a, q_lane0);
       w_st(S, LBW_PT + 0, fp_load(LB_G1X));
       w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
       w_st(S, LBW_PT + 2, a.x.c0);
@@ -1528,7 +1762,7 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
     s_inf = jac_is_inf(Sj) ? 1 : 0;
     if (!s_inf) {
       g2a a;
-      jac_to_aff(a, Sj);
+      g2_to_aff_inl(a, Sj);
       w_st(S, LBW_PT + 0, fp_load(LB_G1X));
       w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
       w_st(S, LBW_PT + 2, a.x.c0);

@@ -13,43 +13,45 @@
 // doubling step on T = (X, Y, Z) (homogeneous projective on the twist), line at P.
 // 25 Fp multiplications: 3b' = 12(1 + u) is applied with additions, and the output is scaled
 // by 4 (a homogeneous (X:Y:Z) ~ (4X:4Y:4Z)) so the textbook halvings of X3, Y3 disappear.
+template <bool kInl = false>
 LB_HD void miller_dbl(g2j& T, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
   fp2 X = T.x, Y = T.y, Z = T.z;
-  fp2 A = fp2_mul(X, Y);             // XY
-  fp2 B = fp2_sqr(Y);
-  fp2 C = fp2_sqr(Z);
+  fp2 A = lean2_mul<kInl>(X, Y);             // XY
+  fp2 B = lean2_sqr<kInl>(Y);
+  fp2 C = lean2_sqr<kInl>(Z);
   fp2 E = fp2_mul3(fp2_dbl(fp2_dbl(fp2_mul_xi(C))));  // 3b' Z^2 = 12 (1 + u) Z^2
   fp2 F = fp2_mul3(E);               // 9b' Z^2
-  fp2 H = fp2_sub(fp2_sqr(fp2_add(Y, Z)), fp2_add(B, C));  // 2YZ
-  fp2 XX3 = fp2_mul3(fp2_sqr(X));
+  fp2 H = fp2_sub(lean2_sqr<kInl>(fp2_add(Y, Z)), fp2_add(B, C));  // 2YZ
+  fp2 XX3 = fp2_mul3(lean2_sqr<kInl>(X));
   // line: (B - E) + (-3X^2 xP) w^2 + (H yP) w^3
   l0 = fp2_sub(B, E);
-  l2 = fp2_neg(fp2_mul_fp(XX3, xP));
-  l3 = fp2_mul_fp(H, yP);
+  l2 = fp2_neg(fp2{lean_mul<kInl>(XX3.c0, xP), lean_mul<kInl>(XX3.c1, xP)});
+  l3 = fp2{lean_mul<kInl>(H.c0, yP), lean_mul<kInl>(H.c1, yP)};
   // 4 x (X3, Y3, Z3) with X3 = XY/2 (B - F), Y3 = ((B+F)/2)^2 - 3E^2, Z3 = B H:
   //   X3' = 2 A (B - F),  Y3' = (B + F)^2 - 12 E^2,  Z3' = 4 B H
-  T.x = fp2_dbl(fp2_mul(A, fp2_sub(B, F)));
-  T.y = fp2_sub(fp2_sqr(fp2_add(B, F)), fp2_mul3(fp2_dbl(fp2_dbl(fp2_sqr(E)))));
-  T.z = fp2_dbl(fp2_dbl(fp2_mul(B, H)));
+  T.x = fp2_dbl(lean2_mul<kInl>(A, fp2_sub(B, F)));
+  T.y = fp2_sub(lean2_sqr<kInl>(fp2_add(B, F)), fp2_mul3(fp2_dbl(fp2_dbl(lean2_sqr<kInl>(E)))));
+  T.z = fp2_dbl(fp2_dbl(lean2_mul<kInl>(B, H)));
 }
 
 // addition step T <- T + Q (Q affine), line through T and Q at P
+template <bool kInl = false>
 LB_HD void miller_add(g2j& T, const g2a& Q, fp2& l0, fp2& l2, fp2& l3, const fp& xP, const fp& yP) {
-  fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
-  fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  fp2 theta = fp2_sub(T.y, lean2_mul<kInl>(Q.y, T.z));
+  fp2 lam = fp2_sub(T.x, lean2_mul<kInl>(Q.x, T.z));
   // line: (theta xQ - lam yQ) + (-theta xP) w^2 + (lam yP) w^3
-  l0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
-  l2 = fp2_neg(fp2_mul_fp(theta, xP));
-  l3 = fp2_mul_fp(lam, yP);
-  fp2 C = fp2_sqr(theta);
-  fp2 D = fp2_sqr(lam);
-  fp2 E = fp2_mul(lam, D);
-  fp2 F = fp2_mul(T.z, C);
-  fp2 G = fp2_mul(T.x, D);
+  l0 = fp2_sub(lean2_mul<kInl>(theta, Q.x), lean2_mul<kInl>(lam, Q.y));
+  l2 = fp2_neg(fp2{lean_mul<kInl>(theta.c0, xP), lean_mul<kInl>(theta.c1, xP)});
+  l3 = fp2{lean_mul<kInl>(lam.c0, yP), lean_mul<kInl>(lam.c1, yP)};
+  fp2 C = lean2_sqr<kInl>(theta);
+  fp2 D = lean2_sqr<kInl>(lam);
+  fp2 E = lean2_mul<kInl>(lam, D);
+  fp2 F = lean2_mul<kInl>(T.z, C);
+  fp2 G = lean2_mul<kInl>(T.x, D);
   fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
-  T.x = fp2_mul(lam, H);
-  T.y = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), fp2_mul(E, T.y));
-  T.z = fp2_mul(T.z, E);
+  T.x = lean2_mul<kInl>(lam, H);
+  T.y = fp2_sub(lean2_mul<kInl>(theta, fp2_sub(G, H)), lean2_mul<kInl>(E, T.y));
+  T.z = lean2_mul<kInl>(T.z, E);
 }
 
 // f_{|x|,Q}(P), conjugated (x < 0).  P, Q affine and not infinity.

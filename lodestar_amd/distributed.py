@@ -4,7 +4,9 @@ ranks; each rank reduces its shard to one 576-byte Fp12 partial product
 the partials are all-gathered (RCCL over xGMI with the "nccl" backend; gloo on CPU in tests),
 and one final exponentiation of their product decides the whole segment.  RCCL has no Fp12
 reduction op, so it is a gather + an on-device product, never an all-reduce.  On a 0 verdict
-every rank localises its own invalid jobs (lb_batch_verify's bisection)."""
+every rank localises its own invalid jobs from the state its partial left on its GPU
+(lb_batch_search_after_partial: the shard's own final exponentiation, then the invalid-set
+search), without re-running the pipeline."""
 from __future__ import annotations
 
 from typing import Callable, List, Sequence, Tuple
@@ -25,7 +27,9 @@ def verify_sharded(partial: Callable[[], Tuple[bytes, Sequence[int]]],
                    product_is_one: Callable[[List[bytes]], bool],
                    local_verify: Callable[[], Sequence[int]],
                    group=None, device=None) -> Tuple[List[int], bool]:
-    """Returns (per-job codes of this rank's shard, global verdict)."""
+    """Returns (per-job codes of this rank's shard, global verdict).  local_verify runs after a
+    failing global verdict: Batch.search_after_partial (continues from this rank's partial) or
+    any full re-verification of the shard."""
     import torch
     import torch.distributed as dist
 

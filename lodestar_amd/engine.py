@@ -142,6 +142,13 @@ class Batch:
                                                 _p(out, ctypes.c_int32)))
         return bytes(buf), out[: self.n_jobs]
 
+    def search_after_partial(self) -> np.ndarray:
+        """Per-job codes from the state the last partial() of this batch left in the engine (the
+        shard's own root check, then the invalid-set search): lb_batch_search_after_partial."""
+        out = np.zeros(max(self.n_jobs, 1), dtype=np.int32)
+        _check(self.engine.lib.lb_batch_search_after_partial(self.engine.h, self.h, _p(out, ctypes.c_int32)))
+        return out[: self.n_jobs]
+
     def free(self):
         if self.h:
             self.engine.lib.lb_batch_destroy(self.h)
@@ -227,10 +234,16 @@ class Engine:
         n = len(keys)
         if n == 0:
             return self.pubkey_table_size(), []
-        size = len(keys[0])
-        if any(len(k) != size for k in keys) or size not in (48, 96):
-            raise ValueError("keys must all be 48 or all be 96 bytes")
-        buf = np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8).copy()
+        if isinstance(keys, np.ndarray) and keys.ndim == 2:  # n x 48 / n x 96 uint8 rows
+            size = int(keys.shape[1])
+            if size not in (48, 96):
+                raise ValueError("keys must all be 48 or all be 96 bytes")
+            buf = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1).copy()
+        else:
+            size = len(keys[0])
+            if any(len(k) != size for k in keys) or size not in (48, 96):
+                raise ValueError("keys must all be 48 or all be 96 bytes")
+            buf = np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8).copy()
         st = np.zeros(n, dtype=np.int32)
         first = ctypes.c_uint32(0)
         _check(self.lib.lb_pubkey_table_append(self.h, n, _p(buf, ctypes.c_uint8), size, 1 if validate else 0,

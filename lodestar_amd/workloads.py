@@ -39,6 +39,9 @@ from .engine import Engine, PackedJobs
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 SEED = 0x4C4F4445
 N_KEYS = 100
+# the distinct-key variant: a mainnet-sized index2pubkey table (~10^6 validators,
+# pubkeyCache.ts:56-77), every validator id of the workloads ([0, 2^20)) its own key
+N_KEYS_MAINNET = 1 << 20
 
 
 def interop_sk(i: int) -> int:
@@ -67,7 +70,9 @@ class Workload:
 class KeyPool:
     def __init__(self, engine: Engine, n: int = N_KEYS):
         self.sks = [interop_sk(i) for i in range(n)]
-        _, self.pk96 = engine.sk_to_pk(self.sks)
+        step = 1 << 16
+        parts = [engine.sk_to_pk(self.sks[a:a + step])[1] for a in range(0, n, step)]
+        self.pk96 = parts[0] if len(parts) == 1 else np.concatenate(parts)
 
     def sk(self, v: int) -> int:
         return self.sks[v % len(self.sks)]
@@ -246,6 +251,8 @@ SPECS = {"c1": c1_specs, "c2": c2_specs, "c3": c3_specs, "c3_distinct": c3_disti
 
 
 def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = SEED, **kw) -> Workload:
+    """`keys`: the key pool validator v draws from (v mod its size); default the reference perf
+    convention's 100 keys, KeyPool(engine, N_KEYS_MAINNET) for the distinct-key variant."""
     rng = np.random.default_rng(seed)
     return build(engine, SPECS[name](rng, **kw), name, keys=keys, seed=seed)
 
@@ -253,7 +260,7 @@ def make(engine: Engine, name: str, keys: Optional[KeyPool] = None, seed: int = 
 def indexed_for(engine: Engine, wl: Workload) -> PackedJobs:
     """Register the workload's key pool in `engine`'s resident table and return the batch with
     4-byte table indices instead of 96-byte keys (the index2pubkey path)."""
-    base, st = engine.pubkey_table_append([r.tobytes() for r in wl.pool96])
+    base, st = engine.pubkey_table_append(np.asarray(wl.pool96, dtype=np.uint8))
     if any(st):
         raise RuntimeError("pubkey table append failed")
     p = wl.packed

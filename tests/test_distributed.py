@@ -118,7 +118,7 @@ def _worker_gpu(rank, world, port, name, out):
         shard.pk_indices = None         # 96-byte keys
         b = eng.upload(shard)
         try:
-            codes, ok = verify_sharded(b.partial, eng.product_is_one, b.verify)
+            codes, ok = verify_sharded(b.partial, eng.product_is_one, b.search_after_partial)
         finally:
             b.free()
         out.put((rank, codes, ok, [int(x) for x in wl.expected[lo:hi]]))
@@ -153,9 +153,32 @@ def test_gloo_two_ranks_gpu_partials_valid():
 
 @pytest.mark.gpu
 def test_gloo_two_ranks_gpu_partials_invalid_localised():
-    """c4 carries wrong and malformed sets: the product check fails on both ranks and each rank's
-    own verify localises its invalid jobs."""
+    """c4 carries wrong and malformed sets: the product check fails on both ranks and each rank
+    localises its invalid jobs from its own partial's state (lb_batch_search_after_partial)."""
     res = _run_gpu("c4")
     assert [ok for _, _, ok, _ in res] == [False, False]
     for _, codes, _, exp in res:
         assert codes == exp
+
+
+@pytest.mark.gpu
+def test_search_after_partial_matches_verify():
+    """lb_batch_search_after_partial (the exchange mode's continuation) gives the per-job codes
+    of lb_batch_verify on a batch with wrong and malformed sets (c4) and on a valid one (c2); a
+    call on the engine in between invalidates the partial's state (LB_ERR_ARGUMENT)."""
+    import numpy as np
+    from lodestar_amd import workloads as W
+    from lodestar_amd.engine import BlsError, Engine
+    with Engine(0) as eng:
+        for name in ("c4", "c2"):
+            wl = W.make(eng, name)
+            b = eng.upload(W.indexed_for(eng, wl))
+            try:
+                _, st = b.partial()
+                assert np.array_equal(b.search_after_partial(), wl.expected), name
+                b.partial()
+                b.verify()
+                with pytest.raises(BlsError):
+                    b.search_after_partial()
+            finally:
+                b.free()

@@ -617,7 +617,10 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     big = str(1 << 31)
     # (all one-lane / MSM forms), (the same with 8-lane Miller loops), (many-lane forms, one-lane
     # S terms), (many-lane forms, 8-lane S terms)
-    for lim, s_g8, mform in (("0", "0", "lane"), ("0", "0", "g8"), (big, "0", "g8"), (big, big, "lane")):
+    # + the bucket MSM's lone-lane bucket sums and reduction (LB_MSM_G8=0) against the 8-lane ones
+    for lim, s_g8, mform, msm_g8 in (("0", "0", "lane", "1"), ("0", "0", "g8", "1"), (big, "0", "g8", "1"),
+                                     (big, big, "lane", "1"), ("0", "0", "lane", "0")):
+        monkeypatch.setenv("LB_MSM_G8", msm_g8)
         monkeypatch.setenv("LB_MILLER_FORM", mform)
         monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
@@ -636,4 +639,4 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
                 b.free()
         assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
         outs.append(part)
-    assert outs[0] == outs[1] == outs[2] == outs[3]
+    assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4]

@@ -2,12 +2,13 @@
 import json
 import sys
 
-d = json.loads(sys.stdin.read().strip().splitlines()[-1])
+src = open(sys.argv[1]) if len(sys.argv) > 1 else sys.stdin
+d = json.loads(src.read().strip().splitlines()[-1])
 r = d["roofline"] or {}
 print("value", d["value"], "single", d["value_one_batch_in_flight"], "distinct", d.get("value_distinct_roots"),
       "ms/step", d["ms_per_step"])
 print(" ".join(f"{k}={v['ms']}" for k, v in r.get("stages", {}).items()))
-for k in ("value_one_invalid_per_batch", "value_e2e", "value_slots1", "latency_slot1_ms", "latency_1set_ms",
+for k in ("value_distinct_keys", "distinct_keys", "value_one_invalid_per_batch", "value_e2e", "value_slots1", "latency_slot1_ms", "latency_1set_ms",
           "latency_block_ms", "value_dropin", "batch_latency_ms", "dropin", "signing_roots"):
     if k in d:
         print(k, d[k])
