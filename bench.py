@@ -52,10 +52,21 @@ sys.path.insert(0, ROOT)
 # Each engine drives three HIP streams; HIP's default of 4 hardware queues per process would make
 # the streams of the batches in flight share queues (false dependencies between independent
 # batches).  24 queues (HIP reads this at runtime init, before any GPU call below) gives each of
-# the 7 engines' 21 streams its own.  Measured on MI355X: profiles/r1_inflight_sweep.txt.  The GPU
+# the 7 engines' 21 streams its own (3 per engine up to 32 for more engines).  Measured on MI355X: profiles/r1_inflight_sweep.txt.  The GPU
 # boxes export GPU_MAX_HW_QUEUES=4, so raise it rather than only defaulting it.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
-    os.environ["GPU_MAX_HW_QUEUES"] = "24"
+def _want_queues():
+    """3 streams per in-flight engine, at least 24, at most 32 (the pool's limit)"""
+    k = 7
+    for i, t in enumerate(sys.argv):
+        if t == "--inflight" and i + 1 < len(sys.argv):
+            k = int(sys.argv[i + 1])
+        elif t.startswith("--inflight="):
+            k = int(t.split("=", 1)[1])
+    return max(24, min(32, 3 * k))
+
+
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _want_queues():
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_want_queues())
 
 import numpy as np  # noqa: E402
 

@@ -114,7 +114,7 @@ struct lb_engine {
       set_live, gacc, gp_aff, gp_inf;
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
-  // k_hash_finish's parked points (4 x 72 words per launched lane)
+  // parked lone-lane state: k_hash_finish's points (4 x 72 words per launched lane), k_miller_lane's T
   dbuf park;
   // the batch whose lb_batch_partial left its state (trees, statuses, scalars) in this engine's
   // workspace, for lb_batch_search_after_partial; any other pipeline run clears it
@@ -576,13 +576,21 @@ struct stage_scope {
 
 // Bucket sums -> S_j = sum_d d B_d per instance j (n_inst instances of W windows, buckets
 // [j W 256, (j+1) W 256) of bsum) -> element out0 + j of `out` (SoA, stride n_out).
+// entries: bucket entries (point, window) of the launch, an upper bound.  The bucket sums go by
+// 8-lane groups (one wave per bucket) only when buckets hold several chunks on average (the batch
+// MSM: ~30 chunk sums per bucket); a search round's many small instances leave ~one chunk per
+// bucket, which one lane per bucket sums without the wave's idle groups.
 static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32_t nb, uint32_t n_inst, int W,
-                             uint32_t* out, uint32_t n_out, uint32_t out0) {
+                             uint32_t* out, uint32_t n_out, uint32_t out0, uint64_t entries) {
   if (e->msm_g8) {
     hipError_t r = e->wsum.ensure((size_t)n_inst * W * sizeof(g2j));
     if (r != hipSuccess) return r;
-    hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(), bcap,
-                       e->bsum.as<uint32_t>(), nb);
+    if (entries >= (uint64_t)4 * LB_GROUP_CHUNK * nb)
+      hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(),
+                         bcap, e->bsum.as<uint32_t>(), nb);
+    else
+      hipLaunchKernelGGL(k_msm_buckets, dim3(nblk(nb)), dim3(LB_TPB), 0, st, e->bch.as<uint32_t>(),
+                         e->bacc.as<uint32_t>(), bcap, e->bsum.as<uint32_t>(), nb);
     hipLaunchKernelGGL(k_msm_window_g8, dim3(n_inst * W), dim3(256), 0, st, e->bsum.as<uint32_t>(), nb,
                        e->wsum.as<uint32_t>(), n_inst * W);
     if (W == LB_MSM_W)
@@ -806,7 +814,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s2, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
-      LB_HIP(msm_reduce(e, s2, bcap, LB_MSM_NB, 1u, LB_MSM_W, e->treeS.as<uint32_t>(), 2 * mj, 1u));
+      LB_HIP(msm_reduce(e, s2, bcap, LB_MSM_NB, 1u, LB_MSM_W, e->treeS.as<uint32_t>(), 2 * mj, 1u,
+                        (uint64_t)2 * LB_MSM_W * n));
     }
     // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
     LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
@@ -827,8 +836,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                            e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
       else if (shared)
+      {
+        LB_HIP(e->park.ensure((size_t)72 * 4 * n));  // T per root (k_hash_finish's parking is done)
         hipLaunchKernelGGL(k_miller_lane, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
-                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>(),
+                           e->park.as<uint32_t>());
+      }
       else
         hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,
                            e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
@@ -1140,7 +1153,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
-      LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u));
+      LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u, (uint64_t)2 * nwin * T));
     }
     if (c)
       hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),

@@ -643,21 +643,113 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 //   * k_miller_g8 (lb_group_exec.h): 8 lanes per root, 32 roots per workgroup, the state in LDS:
 //     ~3x shorter, ~2.5x more VALU work per root; the form for a large batch alone on the device.
 //   * k_miller_wave below: one wave per root, for batches with few distinct roots.
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_miller_lane(uint32_t n, uint32_t m,
-                                                                const uint32_t* __restrict__ n_u,
-                                                                const uint32_t* __restrict__ gp_aff,
-                                                                const uint32_t* __restrict__ gp_inf,
-                                                                const uint32_t* __restrict__ h_aff,
-                                                                uint32_t* __restrict__ treeP) {
+// One lane per root with the Fp12 accumulator f and the tower temporaries in LDS (three 72-word
+// slots per lane, lane-interleaved: 54 KB per wave) and T parked in global memory between the
+// step halves.  Held in registers across ~100 out-of-line product calls per step, f, T, the
+// lines and the temporaries spilled 6.7 KB per lane to the private segment, which the runtime
+// reserves per HIP queue for the device's whole wave capacity (the per-device engine cap).
+typedef __attribute__((address_space(3))) uint32_t lds_w;
+struct lane_lds {
+  lds_w* L;
+  int lane;
+  __device__ __forceinline__ void put(int k, const fp6& v) const {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+    LB_UNROLL for (int i = 0; i < 72; i++) L[(k * 72 + i) * 64 + lane] = w[i];
+    __asm__ volatile("" ::: "memory");
+  }
+  __device__ __forceinline__ fp6 get(int k) const {
+    __asm__ volatile("" ::: "memory");
+    fp6 v;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+    LB_UNROLL for (int i = 0; i < 72; i++) w[i] = L[(k * 72 + i) * 64 + lane];
+    return v;
+  }
+};
+// f <- f^2 = (c0' - t - v t) + 2 t w, t = a0 a1, c0' = (a0 + a1)(a0 + v a1)  (slots 0, 1: f; 2: t)
+__device__ __forceinline__ void lane_f_sqr(const lane_lds& S) {
+  fp6 s1, s2;
+  {
+    const fp6 a0 = S.get(0), a1 = S.get(1);
+    S.put(2, fp6_mul_inl(a0, a1));
+    s1 = fp6_add(a0, a1);
+    s2 = fp6_add(a0, fp6_mul_v(a1));
+  }
+  const fp6 c0 = fp6_mul_inl(s1, s2);
+  const fp6 t = S.get(2);
+  S.put(0, fp6_sub(fp6_sub(c0, t), fp6_mul_v(t)));
+  S.put(1, fp6_add(t, t));
+}
+// f <- f (l0 + l2 v + l3 v w)  (as fp12_mul_line_inl; slot 2 holds t1 = a1 l3)
+__device__ __forceinline__ void lane_f_line(const lane_lds& S, const fp2& l0, const fp2& l2, const fp2& l3) {
+  fp6 s;
+  {
+    const fp6 a1 = S.get(1);
+    S.put(2, fp6_mul_1(a1, l3));
+    const fp6 a0 = S.get(0);
+    s = fp6_add(a0, a1);
+    S.put(0, fp6_mul_01(a0, l0, l2));  // t0 (f.c0 consumed)
+  }
+  const fp6 c1 = fp6_mul_01(s, l0, fp2_add(l2, l3));
+  const fp6 t0 = S.get(0), t1 = S.get(2);
+  S.put(1, fp6_sub(fp6_sub(c1, t0), t1));
+  S.put(0, fp6_add(t0, fp6_mul_v(t1)));
+}
+__global__ void __launch_bounds__(LB_TPB, 1) k_miller_lane(uint32_t n, uint32_t m,
+                                                           const uint32_t* __restrict__ n_u,
+                                                           const uint32_t* __restrict__ gp_aff,
+                                                           const uint32_t* __restrict__ gp_inf,
+                                                           const uint32_t* __restrict__ h_aff,
+                                                           uint32_t* __restrict__ treeP, uint32_t* __restrict__ tpark) {
+  static_assert(LB_TPB == 64, "one wave per block: 64 lanes of LDS slots");
+  __shared__ uint32_t lds[3 * 72 * 64];
   const uint32_t u = lb_tid();
   if (u >= *n_u) return;
-  fp12 f = fp12_one();
+  const lane_lds S{(lds_w*)lds, (int)threadIdx.x};
+  S.put(0, fp6_one());
+  S.put(1, fp6_zero());
   if (!gp_inf[u]) {
-    const g1a p = soa_ld<g1a>(gp_aff, n, u);
-    const g2a h = soa_ld<g2a>(h_aff, n, u);
-    f = miller_loop_inl(p, h);
+    auto park_t = [&](const g2j& T) {
+      soa_st(tpark, n, u, T);
+      __asm__ volatile("" ::: "memory");
+    };
+    auto unpark_t = [&]() {
+      __asm__ volatile("" ::: "memory");
+      return soa_ld<g2j>(tpark, n, u);
+    };
+    {
+      const g2a Q = soa_ld<g2a>(h_aff, n, u);
+      park_t(g2j{Q.x, Q.y, fp2_one()});
+    }
+    bool first = true;
+#pragma clang loop unroll(disable)
+    for (int i = 62; i >= 0; i--) {
+      if (!first) lane_f_sqr(S);
+      first = false;
+      fp2 l0, l2, l3;
+      {
+        g2j T = unpark_t();
+        const g1a P = soa_ld<g1a>(gp_aff, n, u);
+        miller_dbl(T, l0, l2, l3, P.x, P.y);
+        park_t(T);
+      }
+      lane_f_line(S, l0, l2, l3);
+      if ((LB_X_ABS >> i) & 1ull) {
+        {
+          g2j T = unpark_t();
+          const g1a P = soa_ld<g1a>(gp_aff, n, u);
+          miller_add(T, soa_ld<g2a>(h_aff, n, u), l0, l2, l3, P.x, P.y);
+          park_t(T);
+        }
+        lane_f_line(S, l0, l2, l3);
+      }
+    }
+    S.put(1, fp6_neg(S.get(1)));  // conjugate (x < 0)
   }
-  soa_st(treeP, 2 * m, m + u, f);
+  LB_UNROLL for (int h = 0; h < 2; h++) {
+    const fp6 v = S.get(h);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+    LB_UNROLL for (int i = 0; i < 72; i++) treeP[(size_t)(72 * h + i) * (2 * m) + m + u] = w[i];
+  }
 }
 
 __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,

@@ -24,8 +24,13 @@ if [ -n "$PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o $R --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-distinct --no-extra > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
   grep -h '"metric"' $OUT/kt.log | cut -c1-300
 fi
-if [ -n "$ENGINES8" ]; then
-  echo "== 8 engines"
-  LB_MAX_ENGINES_PER_DEVICE=16 timeout -k 10 300 python3 -u bench.py --inflight 8 --steps 10 --warmup 2 --no-cpu-baseline --legs invalid > $OUT/bench8.log 2>&1; rc=$?
-  grep -c OUT_OF_RESOURCES $OUT/bench8.log; tail -1 $OUT/bench8.log | cut -c1-600; echo "rc=$rc"
+if [ -n "$ENGINES" ]; then
+  for N in $ENGINES; do
+    echo "== $N engines"
+    LB_MAX_ENGINES_PER_DEVICE=16 timeout -k 10 300 python3 -u bench.py --inflight $N --steps ${ESTEPS:-10} --warmup 2 --no-cpu-baseline --legs ${ELEGS:-invalid} > $OUT/bench_e$N.log 2>&1; rc=$?
+    echo "OUT_OF_RESOURCES lines: $(grep -c OUT_OF_RESOURCES $OUT/bench_e$N.log)  rc=$rc"
+    tail -1 $OUT/bench_e$N.log > $OUT/bench_e$N.json
+    python3 tools/bench_summary.py $OUT/bench_e$N.json 2>/dev/null | head -4
+    [ $rc -eq 0 ] || exit 1
+  done
 fi
