@@ -271,6 +271,141 @@ __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32
 }
 
 // ---------------------------------------------------------------- hash_to_G2
+// ---- expand_message_xmd for a 32-byte message at word level (no byte buffers: the byte-wise
+// SHA-256 message builder kept its buffers on the stack, ~1.5 KB of private segment per lane).
+// With DST' = DST || 43 (44 bytes), every SHA-256 block but the message's own is constant:
+//   b0 = H(Z_pad || msg || 01 00 || 00 || DST')  blocks: zeros | msg, 01 00 00, DST'[0..28] | DST'[29..43], pad
+//   bi = H((b0 ^ b_{i-1}) || i || DST')         blocks: X, i, DST'[0..30] | DST'[31..43], pad
+typedef uint32_t lb_v8u __attribute__((ext_vector_type(8)));
+static __device__ __attribute__((noinline)) lb_v8u sha256_compress_v(lb_v8u hv, lb_v16u bv) {
+  uint32_t h[8], blk[16];
+  LB_UNROLL for (int i = 0; i < 8; i++) h[i] = hv[i];
+  LB_UNROLL for (int i = 0; i < 16; i++) blk[i] = bv[i];
+  sha256_compress(h, blk);
+  lb_v8u r;
+  LB_UNROLL for (int i = 0; i < 8; i++) r[i] = h[i];
+  return r;
+}
+__device__ __forceinline__ uint32_t dst_byte(int k) { return k < LB_DST_LEN + 1 ? (uint32_t)LB_DST[k] : 0u; }
+__device__ __forceinline__ uint32_t dst_word(int k) {  // big-endian word of DST' bytes [k, k + 4)
+  return (dst_byte(k) << 24) | (dst_byte(k + 1) << 16) | (dst_byte(k + 2) << 8) | dst_byte(k + 3);
+}
+__device__ __forceinline__ lb_v8u sha256_iv_v() {
+  lb_v8u h;
+  h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
+  h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
+  return h;
+}
+// field element u_which (which = 0: bytes [0, 128) of the 256-byte output, 1: [128, 256)) of
+// hash_to_field(msg, 2) for the 32-byte message with big-endian words M
+__device__ __forceinline__ fp2 hash_to_field_u(const uint32_t M[8], int which) {
+  const lb_v8u iv = sha256_iv_v();
+  lb_v16u blk;
+  LB_UNROLL for (int i = 0; i < 16; i++) blk[i] = 0u;
+  lb_v8u b0 = sha256_compress_v(iv, blk);  // the zero block Z_pad
+  LB_UNROLL for (int i = 0; i < 8; i++) blk[i] = M[i];
+  blk[8] = 0x01000000u | dst_byte(0);
+  LB_UNROLL for (int i = 9; i < 16; i++) blk[i] = dst_word(4 * i - 35);
+  b0 = sha256_compress_v(b0, blk);
+  LB_UNROLL for (int i = 0; i < 4; i++) blk[i] = dst_word(29 + 4 * i);
+  blk[3] = (dst_byte(41) << 24) | (dst_byte(42) << 16) | (dst_byte(43) << 8) | 0x80u;
+  LB_UNROLL for (int i = 4; i < 15; i++) blk[i] = 0u;
+  blk[15] = 143u * 8u;
+  b0 = sha256_compress_v(b0, blk);
+  uint32_t out[32];
+  lb_v8u prev = b0 ^ b0;  // zero
+  LB_UNROLL for (int i = 1; i <= 8; i++) {
+    if ((i - 1) / 4 > which) break;  // later blocks belong to the other element
+    lb_v16u bb;
+    LB_UNROLL for (int k = 0; k < 8; k++) bb[k] = b0[k] ^ prev[k];
+    bb[8] = ((uint32_t)i << 24) | (dst_byte(0) << 16) | (dst_byte(1) << 8) | dst_byte(2);
+    LB_UNROLL for (int k = 9; k < 16; k++) bb[k] = dst_word(4 * k - 33);
+    lb_v8u bi = sha256_compress_v(iv, bb);
+    LB_UNROLL for (int k = 0; k < 3; k++) bb[k] = dst_word(31 + 4 * k);
+    bb[3] = (dst_byte(43) << 24) | 0x00800000u;
+    LB_UNROLL for (int k = 4; k < 15; k++) bb[k] = 0u;
+    bb[15] = 77u * 8u;
+    bi = sha256_compress_v(bi, bb);
+    prev = bi;
+    if ((i - 1) / 4 == which) LB_UNROLL for (int k = 0; k < 8; k++) out[8 * ((i - 1) & 3) + k] = bi[k];
+  }
+  return fp2{fp_from_be64_words(out), fp_from_be64_words(out + 16)};
+}
+// inline pieces of map_to_curve_g2 (register arguments only: by-value structs go through the stack)
+__device__ __forceinline__ fp2 fp2_inv_i(const fp2& a) {
+  const fp ni = fp_inv_i(fp_add(fp_sqr(a.c0), fp_sqr(a.c1)));
+  return fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+__device__ __forceinline__ bool fp_is_square_i(const fp& a) {
+  if (fp_is_zero(a)) return true;
+  uint32_t u[12], v[12];
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    u[j] = a.v[j];
+    v[j] = Pl[j];
+  }
+  int t = 1;  // as fp_is_square (binary Jacobi symbol on the Montgomery form)
+  while (true) {
+    while (u[0] == 0) {
+      LB_UNROLL for (int j = 0; j < 11; j++) u[j] = u[j + 1];
+      u[11] = 0;
+    }
+    int k = lb_ctz32(u[0]);
+    if (k) {
+      lb_shr(u, k);
+      uint32_t v8 = v[0] & 7u;
+      if ((k & 1) && (v8 == 3u || v8 == 5u)) t = -t;
+    }
+    if (lb_is_one_plain(u)) return t == 1;
+    if (!lb_geq(u, v)) {
+      if ((u[0] & 3u) == 3u && (v[0] & 3u) == 3u) t = -t;
+      LB_UNROLL for (int j = 0; j < 12; j++) {
+        uint32_t x = u[j];
+        u[j] = v[j];
+        v[j] = x;
+      }
+      if (lb_is_one_plain(u)) return t == 1;
+    }
+    lb_sub_in(u, v);
+    bool zero = true;
+    LB_UNROLL for (int j = 0; j < 12; j++) zero &= u[j] == 0;
+    if (zero) return false;
+  }
+}
+// map_to_curve_g2 (SSWU + 3-isogeny, lb_h2c.h) with the inline pieces above
+__device__ __forceinline__ g2j map_to_curve_g2_i(const fp2& u) {
+  const fp2 A = fp2_load(LB_SSWU_A), B = fp2_load(LB_SSWU_B), Z = fp2_load(LB_SSWU_Z);
+  const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
+  const fp2 tv1 = fp2_add(fp2_sqr(zu2), zu2);
+  const bool exc = fp2_is_zero(tv1);
+  fp2 x1 = fp2_mul(fp2_load(LB_SSWU_MBDIVA), fp2_add(fp2_one(), fp2_inv_i(tv1)));
+  x1 = fp2_select(exc, fp2_load(LB_SSWU_BDIVZA), x1);
+  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
+  const fp2 x2 = fp2_mul(zu2, x1);
+  const fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), A), x2), B);
+  const bool sq1 = fp_is_square_i(fp_add(fp_sqr(gx1.c0), fp_sqr(gx1.c1)));
+  const fp2 x = fp2_select(sq1, x1, x2);
+  fp2 y;
+  fp2_sqrt_i<true>(y, fp2_select(sq1, gx1, gx2));
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  const fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
+  const fp2 xn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_XNUM3), xxx), fp2_mul(fp2_load(LB_ISO_XNUM2), xx)),
+                                 fp2_mul(fp2_load(LB_ISO_XNUM1), x)),
+                         fp2_load(LB_ISO_XNUM0));
+  const fp2 xd = fp2_add(fp2_add(xx, fp2_mul(fp2_load(LB_ISO_XDEN1), x)), fp2_load(LB_ISO_XDEN0));
+  const fp2 yn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_YNUM3), xxx), fp2_mul(fp2_load(LB_ISO_YNUM2), xx)),
+                                 fp2_mul(fp2_load(LB_ISO_YNUM1), x)),
+                         fp2_load(LB_ISO_YNUM0));
+  const fp2 yd = fp2_add(fp2_add(fp2_add(xxx, fp2_mul(fp2_load(LB_ISO_YDEN2), xx)), fp2_mul(fp2_load(LB_ISO_YDEN1), x)),
+                         fp2_load(LB_ISO_YDEN0));
+  g2j r;
+  const fp2 yd2 = fp2_sqr(yd);
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
+  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(fp2_sqr(xd), xd)), yd2);
+  return r;
+}
+
 // Hashing runs once per DISTINCT signing root (k_msg_insert below): launched over 2 nu threads
 // (nu = distinct roots, read back by the host); thread t handles unique message t % nu, field
 // element u_{t / nu}; output Jacobian points q (stride 2n: u_0 of root u at u, u_1 at n + u).
@@ -281,14 +416,14 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32
   if (t >= 2 * nu) return;
   const uint32_t which = t < nu ? 0u : 1u;
   const uint32_t u = which ? t - nu : t;
-  uint8_t m[32];
-  ld_bytes<32>(m, msgs + (size_t)32 * uniq_set[u]);
-  uint32_t ub[64];
-  expand_message_xmd_256(ub, m);
-  const uint32_t* w = ub + 32 * which;
-  fp2 u2{fp_from_be64_words(w), fp_from_be64_words(w + 16)};
-  g2j p = map_to_curve_g2(u2);
-  soa_st(q, 2 * n, which * n + u, p);
+  const uint4* m4 = reinterpret_cast<const uint4*>(msgs + (size_t)32 * uniq_set[u]);
+  uint32_t M[8];
+  LB_UNROLL for (int i = 0; i < 2; i++) {
+    const uint4 v = m4[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    LB_UNROLL for (int k = 0; k < 4; k++) M[4 * i + k] = __builtin_bswap32(w[k]);  // big-endian words
+  }
+  soa_st(q, 2 * n, which * n + u, map_to_curve_g2_i(hash_to_field_u(M, (int)which)));
 }
 
 // Lone-lane state parked in an engine-owned global buffer (word w of slot k of root u at
