@@ -134,6 +134,9 @@ struct lb_engine {
   // LB_MILLER_FORM = lane | g8 pins the large-batch form (default: by device load).
   uint32_t miller_wave_max = 2048;
   int miller_form = 0;  // 0 by load, 1 lane, 2 g8
+  // one-lane Miller loops with f and a temporary in LDS (two waves per CU) up to this many roots,
+  // f alone in LDS (one wave per SIMD) above: LB_MILLER_LDS3_MAX (lb_kernels.h k_miller_lane)
+  uint32_t miller_lds3_max = 32768;
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
@@ -182,6 +185,9 @@ struct lb_engine {
 // Engines per device are capped so that one process cannot create more concurrently active
 // HIP streams than the device can back with queues and scratch (exhaustion aborts the HSA queue
 // asynchronously instead of returning an error).  LB_MAX_ENGINES_PER_DEVICE overrides the cap.
+// Round 4: 16 (was 7).  Every queue's scratch is reserved for the largest private segment it runs
+// times the device's wave capacity; with the per-root kernels at <= 1.3 KB per lane (k_miller_lane
+// was 6.7 KB) 8 and 10 engines run without an abort (profiles/r4_engines_ab.txt).
 static std::mutex g_engine_mu;
 static int g_engine_count[64];
 // Batches currently inside the pipeline per device (all engines of the process).  With more than
@@ -198,7 +204,7 @@ struct busy_scope {
 static int max_engines_per_device() {
   const char* v = getenv("LB_MAX_ENGINES_PER_DEVICE");
   int k = v ? atoi(v) : 0;
-  return k > 0 ? k : 7;
+  return k > 0 ? k : 16;
 }
 
 #define LB_HIP(call)                                                                        \
@@ -294,6 +300,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
+  if (const char* ml = getenv("LB_MILLER_LDS3_MAX")) e->miller_lds3_max = (uint32_t)strtoul(ml, nullptr, 10);
   if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
@@ -837,10 +844,15 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                            e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
       else if (shared)
       {
-        LB_HIP(e->park.ensure((size_t)72 * 4 * n));  // T per root (k_hash_finish's parking is done)
-        hipLaunchKernelGGL(k_miller_lane, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
-                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>(),
-                           e->park.as<uint32_t>());
+        LB_HIP(e->park.ensure((size_t)2 * 72 * 4 * n));  // T and a temporary per root
+        if (nuh <= e->miller_lds3_max)
+          hipLaunchKernelGGL(k_miller_lane<3>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu,
+                             e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
+                             e->treeP.as<uint32_t>(), e->park.as<uint32_t>());
+        else
+          hipLaunchKernelGGL(k_miller_lane<2>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu,
+                             e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
+                             e->treeP.as<uint32_t>(), e->park.as<uint32_t>());
       }
       else
         hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,

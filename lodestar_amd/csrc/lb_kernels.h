@@ -778,30 +778,44 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 //   * k_miller_g8 (lb_group_exec.h): 8 lanes per root, 32 roots per workgroup, the state in LDS:
 //     ~3x shorter, ~2.5x more VALU work per root; the form for a large batch alone on the device.
 //   * k_miller_wave below: one wave per root, for batches with few distinct roots.
-// One lane per root with the Fp12 accumulator f and the tower temporaries in LDS (three 72-word
-// slots per lane, lane-interleaved: 54 KB per wave) and T parked in global memory between the
-// step halves.  Held in registers across ~100 out-of-line product calls per step, f, T, the
-// lines and the temporaries spilled 6.7 KB per lane to the private segment, which the runtime
-// reserves per HIP queue for the device's whole wave capacity (the per-device engine cap).
+// One lane per root with the Fp12 accumulator f in LDS (two 72-word slots per lane,
+// lane-interleaved: 36 KB per wave, so LDS allows the same one wave per SIMD as the registers)
+// and T and a tower temporary parked in global memory.  Held in registers across ~100
+// out-of-line product calls per step, f, T, the lines and the temporaries spilled 6.7 KB per
+// lane to the private segment, which the runtime reserves per HIP queue for the device's whole
+// wave capacity (the per-device engine cap).
+#ifndef LB_MILLER_LANE_REG
+#define LB_MILLER_LANE_REG 0
+#endif
 typedef __attribute__((address_space(3))) uint32_t lds_w;
+template <int NL>  // slots [0, NL) in LDS (2: f; 3: f and the temporary), the rest in global memory
 struct lane_lds {
-  lds_w* L;
+  lds_w* L;         // slots 0, 1: f.c0, f.c1
+  uint32_t* g;      // slot 2 (a temporary) and slot 3 (T): word i of slot k at g[((k - 2) * 72 + i) * n + u]
+  uint32_t n, u;
   int lane;
   __device__ __forceinline__ void put(int k, const fp6& v) const {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
-    LB_UNROLL for (int i = 0; i < 72; i++) L[(k * 72 + i) * 64 + lane] = w[i];
+    if (k < NL)
+      LB_UNROLL for (int i = 0; i < 72; i++) L[(k * 72 + i) * 64 + lane] = w[i];
+    else
+      LB_UNROLL for (int i = 0; i < 72; i++) g[((size_t)(k - 2) * 72 + i) * n + u] = w[i];
     __asm__ volatile("" ::: "memory");
   }
   __device__ __forceinline__ fp6 get(int k) const {
     __asm__ volatile("" ::: "memory");
     fp6 v;
     uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-    LB_UNROLL for (int i = 0; i < 72; i++) w[i] = L[(k * 72 + i) * 64 + lane];
+    if (k < NL)
+      LB_UNROLL for (int i = 0; i < 72; i++) w[i] = L[(k * 72 + i) * 64 + lane];
+    else
+      LB_UNROLL for (int i = 0; i < 72; i++) w[i] = g[((size_t)(k - 2) * 72 + i) * n + u];
     return v;
   }
 };
 // f <- f^2 = (c0' - t - v t) + 2 t w, t = a0 a1, c0' = (a0 + a1)(a0 + v a1)  (slots 0, 1: f; 2: t)
-__device__ __forceinline__ void lane_f_sqr(const lane_lds& S) {
+template <class S_t>
+__device__ __forceinline__ void lane_f_sqr(const S_t& S) {
   fp6 s1, s2;
   {
     const fp6 a0 = S.get(0), a1 = S.get(1);
@@ -815,7 +829,8 @@ __device__ __forceinline__ void lane_f_sqr(const lane_lds& S) {
   S.put(1, fp6_add(t, t));
 }
 // f <- f (l0 + l2 v + l3 v w)  (as fp12_mul_line_inl; slot 2 holds t1 = a1 l3)
-__device__ __forceinline__ void lane_f_line(const lane_lds& S, const fp2& l0, const fp2& l2, const fp2& l3) {
+template <class S_t>
+__device__ __forceinline__ void lane_f_line(const S_t& S, const fp2& l0, const fp2& l2, const fp2& l3) {
   fp6 s;
   {
     const fp6 a1 = S.get(1);
@@ -829,27 +844,36 @@ __device__ __forceinline__ void lane_f_line(const lane_lds& S, const fp2& l0, co
   S.put(1, fp6_sub(fp6_sub(c1, t0), t1));
   S.put(0, fp6_add(t0, fp6_mul_v(t1)));
 }
+// NL = 3 (f and the temporary in LDS, 54 KB per wave: two waves per CU) keeps the per-root chain
+// fastest; NL = 2 (36 KB: one wave per SIMD, as the registers allow) for batches of so many
+// distinct roots that the LDS bound would leave most of them waiting (lb_engine.hip).
+template <int NL>
 __global__ void __launch_bounds__(LB_TPB, 1) k_miller_lane(uint32_t n, uint32_t m,
                                                            const uint32_t* __restrict__ n_u,
                                                            const uint32_t* __restrict__ gp_aff,
                                                            const uint32_t* __restrict__ gp_inf,
                                                            const uint32_t* __restrict__ h_aff,
                                                            uint32_t* __restrict__ treeP, uint32_t* __restrict__ tpark) {
-  static_assert(LB_TPB == 64, "one wave per block: 64 lanes of LDS slots");
-  __shared__ uint32_t lds[3 * 72 * 64];
+#if LB_MILLER_LANE_REG  // A/B builds only: the round-3 register-resident kernel (6.7 KB private segment)
   const uint32_t u = lb_tid();
   if (u >= *n_u) return;
-  const lane_lds S{(lds_w*)lds, (int)threadIdx.x};
+  fp12 f = fp12_one();
+  if (!gp_inf[u]) f = miller_loop_inl(soa_ld<g1a>(gp_aff, n, u), soa_ld<g2a>(h_aff, n, u));
+  soa_st(treeP, 2 * m, m + u, f);
+  (void)tpark;
+#else
+  static_assert(LB_TPB == 64, "one wave per block: 64 lanes of LDS slots");
+  __shared__ uint32_t lds[NL * 72 * 64];
+  const uint32_t u = lb_tid();
+  if (u >= *n_u) return;
+  const lane_lds<NL> S{(lds_w*)lds, tpark, n, u, (int)threadIdx.x};
   S.put(0, fp6_one());
   S.put(1, fp6_zero());
   if (!gp_inf[u]) {
-    auto park_t = [&](const g2j& T) {
-      soa_st(tpark, n, u, T);
-      __asm__ volatile("" ::: "memory");
-    };
+    auto park_t = [&](const g2j& T) { S.put(3, *reinterpret_cast<const fp6*>(&T)); };
     auto unpark_t = [&]() {
-      __asm__ volatile("" ::: "memory");
-      return soa_ld<g2j>(tpark, n, u);
+      const fp6 v = S.get(3);
+      return *reinterpret_cast<const g2j*>(&v);
     };
     {
       const g2a Q = soa_ld<g2a>(h_aff, n, u);
@@ -885,6 +909,7 @@ __global__ void __launch_bounds__(LB_TPB, 1) k_miller_lane(uint32_t n, uint32_t 
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
     LB_UNROLL for (int i = 0; i < 72; i++) treeP[(size_t)(72 * h + i) * (2 * m) + m + u] = w[i];
   }
+#endif
 }
 
 __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,

@@ -617,10 +617,13 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
     big = str(1 << 31)
     # (all one-lane / MSM forms), (the same with 8-lane Miller loops), (many-lane forms, one-lane
     # S terms), (many-lane forms, 8-lane S terms)
-    # + the bucket MSM's lone-lane bucket sums and reduction (LB_MSM_G8=0) against the 8-lane ones
-    for lim, s_g8, mform, msm_g8 in (("0", "0", "lane", "1"), ("0", "0", "g8", "1"), (big, "0", "g8", "1"),
-                                     (big, big, "lane", "1"), ("0", "0", "lane", "0")):
+    # + the bucket MSM's lone-lane bucket sums and reduction (LB_MSM_G8=0) against the 8-lane ones,
+    # + the one-lane Miller loop with f alone in LDS (LB_MILLER_LDS3_MAX=0: k_miller_lane<2>)
+    for lim, s_g8, mform, msm_g8, lds3 in (("0", "0", "lane", "1", big), ("0", "0", "g8", "1", big),
+                                           (big, "0", "g8", "1", big), (big, big, "lane", "1", big),
+                                           ("0", "0", "lane", "0", big), ("0", "0", "lane", "1", "0")):
         monkeypatch.setenv("LB_MSM_G8", msm_g8)
+        monkeypatch.setenv("LB_MILLER_LDS3_MAX", lds3)
         monkeypatch.setenv("LB_MILLER_FORM", mform)
         monkeypatch.setenv("LB_MILLER_WAVE_MAX", lim)
         monkeypatch.setenv("LB_HASH_G8_MAX", lim)
@@ -639,4 +642,4 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
                 b.free()
         assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
         outs.append(part)
-    assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4]
+    assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4] == outs[5]

@@ -22,7 +22,8 @@ STAGES = {
     "hash_finish": ["k_hash_finish", "k_hash_finish_g8"],
     "pk_chunks": ["k_pk_chunks", "k_pk_chunks_idx"],
     "pk_blind": ["k_pk_blind"],
-    "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
+    "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce", "k_msm_buckets_g8",
+                "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind", "k_sig_blind_g8", "k_g2_sum64"],
     "group_sum": ["k_gsum_chunks", "k_gsum_final"],
     "miller": ["k_miller_g8", "k_miller_lane", "k_miller_wave"],
     "tree_up_P": ["k_tree_up_U"],
@@ -43,8 +44,17 @@ def per_kernel(path, counter):
 def main():
     fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
     n = int(sys.argv[3])
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE (separate passes), bench.py --inflight 1",
+    inflight = sys.argv[4] if len(sys.argv) > 4 else "1"
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE (separate passes), bench.py --inflight {inflight}",
            "unit": "bytes per launch (kernels) / per batch (stages)", "kernels": {}, "stages": {}}
+    # calibration on a kernel with a known byte count: k_msg_insert reads each set's 32-byte root
+    # as two 16-byte loads per lane (plus ~one 4-byte table probe per set) and writes 4 B per set
+    if "k_msg_insert" in fetch:
+        f = sum(fetch["k_msg_insert"]) / len(fetch["k_msg_insert"]) * 1024
+        out["calibration"] = {"kernel": "k_msg_insert", "known_read_bytes": 32 * n, "probe_bytes_about": 4 * n,
+                              "fetch_bytes": round(f), "fetch_over_known": round(f / (32 * n), 3),
+                              "note": "MI355X_MICROARCH.md: FETCH_SIZE counts half of a 16 B/lane streaming read; "
+                                      "the stage totals below are raw FETCH_SIZE + WRITE_SIZE"}
     for k in sorted(set(fetch) & set(write)):
         if not k.startswith("k_"):
             continue
