@@ -116,6 +116,13 @@ struct lb_engine {
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
   // parked lone-lane state: k_hash_finish's points (4 x 72 words per launched lane), k_miller_lane's T
   dbuf park;
+  // per-root chain on speculative liveness (pubkey statuses only), started after the pubkey side
+  // instead of after the signature decode; redone with the full statuses only when a set's
+  // signature failed to decode (k_live_mismatch).  LB_SPEC_GSUM=1; off by default: measured no
+  // gain, the streams then contend for a chip one batch already fills (profiles/r4_spec_ab.txt)
+  bool spec_gsum = false;
+  dbuf set_spec, live_flag;
+  uint32_t* h_flag = nullptr;
   // the batch whose lb_batch_partial left its state (trees, statuses, scalars) in this engine's
   // workspace, for lb_batch_search_after_partial; any other pipeline run clears it
   lb_batch* partial_batch = nullptr;
@@ -313,13 +320,16 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
+  if (const char* sm = getenv("LB_SPEC_GSUM")) e->spec_gsum = std::atoi(sm) != 0;
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_flag, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
     if (e->stream3) hipStreamDestroy(e->stream3);
+    if (e->h_nu) hipHostFree(e->h_nu);
     delete e;
     std::lock_guard<std::mutex> lk(g_engine_mu);
     g_engine_count[device]--;
@@ -348,7 +358,7 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
-                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->wsum, &e->park, &e->pk_aff, &e->y_root, &e->kzg_g1,
+                  &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->wsum, &e->park, &e->set_spec, &e->live_flag, &e->pk_aff, &e->y_root, &e->kzg_g1,
                   &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
@@ -365,6 +375,7 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamSynchronize(e->stream3);
   if (e->scratch) delete e->scratch;
   if (e->h_nu) hipHostFree(e->h_nu);
+  if (e->h_flag) hipHostFree(e->h_flag);
   hipStreamDestroy(e->stream2);
   hipStreamDestroy(e->stream3);
   hipStreamDestroy(e->stream);
@@ -588,11 +599,11 @@ struct stage_scope {
 // MSM: ~30 chunk sums per bucket); a search round's many small instances leave ~one chunk per
 // bucket, which one lane per bucket sums without the wave's idle groups.
 static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32_t nb, uint32_t n_inst, int W,
-                             uint32_t* out, uint32_t n_out, uint32_t out0, uint64_t entries) {
+                             uint32_t* out, uint32_t n_out, uint32_t out0, uint64_t entries, uint32_t chunk) {
   if (e->msm_g8) {
     hipError_t r = e->wsum.ensure((size_t)n_inst * W * sizeof(g2j));
     if (r != hipSuccess) return r;
-    if (entries >= (uint64_t)4 * LB_GROUP_CHUNK * nb)
+    if (entries >= (uint64_t)4 * chunk * nb)
       hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(),
                          bcap, e->bsum.as<uint32_t>(), nb);
     else
@@ -616,6 +627,52 @@ static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32
   else
     hipLaunchKernelGGL(k_msm_reduce<LB_SMSM_W>, dim3(n_inst), dim3(64 * LB_SMSM_W), 0, st, e->bsum.as<uint32_t>(), nb,
                        out, n_out, out0);
+  return hipGetLastError();
+}
+
+// s1: P_u = sum of r_i PK_i over the sets of root u with live[i] (k_gsum_*), the Miller loops
+// (form by root count and device load) into the leaves of the root product tree, the tree.
+static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_t mu, const uint32_t* live) {
+  hipStream_t s1 = e->stream;
+  const uint32_t* nu = e->n_u.as<uint32_t>();
+  {
+    stage_scope sc(e, ST_GSUM, s1);
+    // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
+    hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nuh + n / LB_GROUP_CHUNK)), dim3(LB_TPB), 0, s1, n, nu,
+                       e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
+                       e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
+    hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                       e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
+  }
+  {
+    stage_scope sc(e, ST_MILLER, s1);
+    const bool shared = e->miller_form == 1 ||
+                        (e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1);
+    if (nuh <= e->miller_wave_max) {
+      hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                         e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+    } else if (shared) {
+      hipError_t r = e->park.ensure((size_t)2 * 72 * 4 * n);  // T and a temporary per root
+      if (r != hipSuccess) return r;
+      if (nuh <= e->miller_lds3_max)
+        hipLaunchKernelGGL(k_miller_lane<3>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>(),
+                           e->park.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_miller_lane<2>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>(),
+                           e->park.as<uint32_t>());
+    } else {
+      hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,
+                         e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
+                         e->treeP.as<uint32_t>());
+    }
+  }
+  {
+    stage_scope sc(e, ST_TREE_P, s1);
+    for (uint32_t lo = mu / 2; lo >= 1; lo /= 2)
+      hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
+  }
   return hipGetLastError();
 }
 
@@ -657,7 +714,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->n_u.ensure(4));
   LB_HIP(e->gacc.ensure((size_t)ns * sizeof(g1j)));
   LB_HIP(e->gp_aff.ensure((size_t)ns * sizeof(g1a)));
-  const uint32_t bcap = (2 * LB_MSM_W * ns) / LB_GROUP_CHUNK + LB_MSM_NB;  // bucket chunks, upper bound
+  const uint32_t bcap = (2 * LB_MSM_W * ns) / LB_MSM_CHUNK + LB_MSM_NB;  // bucket chunks, upper bound
   LB_HIP(e->sig_aos.ensure((size_t)ns * sizeof(g2a)));
   LB_HIP(e->bcnt.ensure((size_t)LB_MSM_NB * 4));
   LB_HIP(e->bcursor.ensure((size_t)LB_MSM_NB * 4));
@@ -692,7 +749,9 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // two would contend with the per-root chain on s1 for the whole chip
     // (also for a large batch alone on the device: its s1 chain then slowed by more than the s2
     // chain gained, 5.2 -> 5.1 M sets/s, round-3 A/B)
-    const hipStream_t s3 = n <= e->small_s_max ? s3_ : s2;
+    // (with the speculative per-root chain the pubkey side always runs on s3: the chain starts
+    // when it is done, beside the decode)
+    const hipStream_t s3 = (e->spec_gsum || n <= e->small_s_max) ? s3_ : s2;
     {
       stage_scope sc(e, ST_PK_CHUNKS, s3);
       if (nc && b->indexed)
@@ -747,7 +806,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
                          e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
                          e->gpos.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, (uint32_t)LB_GROUP_CHUNK, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
                          e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
@@ -812,7 +871,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       LB_HIP(hipMemsetAsync(e->bcursor.p, 0, (size_t)LB_MSM_NB * 4, s2));
       hipLaunchKernelGGL(k_msm_count, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
                          e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s2, nullptr, (uint32_t)LB_MSM_NB, e->bcnt.as<uint32_t>(),
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s2, nullptr, (uint32_t)LB_MSM_NB, (uint32_t)LB_MSM_CHUNK,
+                         e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
                          e->bchunk_end.as<uint32_t>());
       hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
@@ -822,47 +882,19 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), (uint32_t)LB_MSM_NB);
       LB_HIP(msm_reduce(e, s2, bcap, LB_MSM_NB, 1u, LB_MSM_W, e->treeS.as<uint32_t>(), 2 * mj, 1u,
-                        (uint64_t)2 * LB_MSM_W * n));
+                        (uint64_t)2 * LB_MSM_W * n, LB_MSM_CHUNK));
     }
-    // ---- s1: per-root sums of r_i PK_i over live jobs' sets (needs the statuses from s2)
-    LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
-    {
-      stage_scope sc(e, ST_GSUM, s1);
-      // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
-      hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nuh + n / LB_GROUP_CHUNK)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
-                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(),
-                         e->set_live.as<uint32_t>(), e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
-      hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
-                         e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
-    }
-    {
-      stage_scope sc(e, ST_MILLER, s1);
-      const bool shared = e->miller_form == 1 ||
-                          (e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1);
-      if (nuh <= e->miller_wave_max)
-        hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
-                           e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
-      else if (shared)
-      {
-        LB_HIP(e->park.ensure((size_t)2 * 72 * 4 * n));  // T and a temporary per root
-        if (nuh <= e->miller_lds3_max)
-          hipLaunchKernelGGL(k_miller_lane<3>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu,
-                             e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
-                             e->treeP.as<uint32_t>(), e->park.as<uint32_t>());
-        else
-          hipLaunchKernelGGL(k_miller_lane<2>, dim3(nblk(nuh)), dim3(LB_TPB), 0, s1, n, mu, nu,
-                             e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
-                             e->treeP.as<uint32_t>(), e->park.as<uint32_t>());
-      }
-      else
-        hipLaunchKernelGGL(k_miller_g8, dim3((nuh + LBG_ROOTS - 1) / LBG_ROOTS), dim3(64 * LBG_WAVES), 0, s1, n, mu, nu,
-                           e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(),
-                           e->treeP.as<uint32_t>());
-    }
-    {
-      stage_scope sc(e, ST_TREE_P, s1);
-      for (uint32_t lo = mu / 2; lo >= 1; lo /= 2)
-        hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
+    // ---- s1: per-root sums of r_i PK_i and the Miller loops: on speculative liveness (the pubkey
+    // side only) as soon as it is done, else after the signature decode
+    if (e->spec_gsum) {
+      LB_HIP(e->set_spec.ensure((size_t)ns * 4));
+      LB_HIP(hipStreamWaitEvent(s1, e->ev_pk, 0));
+      hipLaunchKernelGGL(k_spec_live, dim3(nblk(nj)), dim3(LB_TPB), 0, s1, nj, b->d_job_off.as<uint32_t>(),
+                         e->pk_status.as<int32_t>(), e->set_spec.as<uint32_t>());
+      LB_HIP(per_root_chain(e, n, nuh, mu, e->set_spec.as<uint32_t>()));
+    } else {
+      LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
+      LB_HIP(per_root_chain(e, n, nuh, mu, e->set_live.as<uint32_t>()));
     }
   } else {
     // no sets: every job is empty; the message tree is the single identity leaf
@@ -884,6 +916,17 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(hipEventRecord(e->ev_s, s2));
   LB_HIP(hipStreamWaitEvent(s1, e->ev_s, 0));  // join
   LB_HIP(hipGetLastError());
+  if (n && e->spec_gsum) {
+    // a set counted in the speculative sums whose signature failed to decode: redo the per-root
+    // chain with the full statuses (batches with malformed signatures only)
+    LB_HIP(e->live_flag.ensure(4));
+    LB_HIP(hipMemsetAsync(e->live_flag.p, 0, 4, s1));
+    hipLaunchKernelGGL(k_live_mismatch, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_live.as<uint32_t>(),
+                       e->set_spec.as<uint32_t>(), e->live_flag.as<uint32_t>());
+    LB_HIP(hipMemcpyAsync(e->h_flag, e->live_flag.p, 4, hipMemcpyDeviceToHost, s1));
+    LB_HIP(hipStreamSynchronize(s1));
+    if (*e->h_flag) LB_HIP(per_root_chain(e, n, *e->h_nu, mu, e->set_live.as<uint32_t>()));
+  }
   return LB_OK;
 }
 
@@ -1147,7 +1190,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
                              e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
                              e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
       }
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, e->bcnt.as<uint32_t>(),
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, (uint32_t)LB_GROUP_CHUNK, e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
                          e->bchunk_end.as<uint32_t>());
       if (T) {
@@ -1165,7 +1208,8 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       hipLaunchKernelGGL(k_msm_chunks, dim3(nblk(bcap)), dim3(LB_TPB), 0, s1, e->bch.as<uint32_t>(),
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
-      LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u, (uint64_t)2 * nwin * T));
+      LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u, (uint64_t)2 * nwin * T,
+                        LB_GROUP_CHUNK));
     }
     if (c)
       hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),

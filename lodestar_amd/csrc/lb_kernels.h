@@ -948,6 +948,9 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // roots cannot be aimed at one probe chain); equality is decided on all 32 bytes.  A slot, once
 // claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
 #define LB_GROUP_CHUNK 32  // members summed per lane in k_gsum_chunks
+#ifndef LB_MSM_CHUNK
+#define LB_MSM_CHUNK 16  // bucket members summed per lane in k_msm_chunks (the batch MSM's serial chain)
+#endif
 __device__ __forceinline__ bool msg_eq(const uint8_t* __restrict__ msgs, uint32_t a, uint32_t b) {
   const uint4* x = reinterpret_cast<const uint4*>(msgs + (size_t)32 * a);
   const uint4* y = reinterpret_cast<const uint4*>(msgs + (size_t)32 * b);
@@ -1025,7 +1028,7 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t
 // One block: exclusive scans of the group sizes (member offsets goff) and of their chunk
 // counts (gch), and the member range of every chunk.  goff[n_u] / gch[n_u] = totals.
 // (n_u == nullptr: nu_const groups; the MSM's buckets use it too)
-__global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, uint32_t nu_const,
+__global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, uint32_t nu_const, uint32_t chunk,
                                                    const uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ gch,
                                                    uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end) {
@@ -1035,7 +1038,7 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
   uint32_t sm = 0, sc = 0;
   for (uint32_t u = a; u < b; u++) {
     sm += cnt[u];
-    sc += (cnt[u] + LB_GROUP_CHUNK - 1) / LB_GROUP_CHUNK;
+    sc += (cnt[u] + chunk - 1) / chunk;
   }
   s_m[t] = sm;
   s_c[t] = sc;
@@ -1052,9 +1055,9 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     const uint32_t c = cnt[u];
     goff[u] = om;
     gch[u] = oc;
-    for (uint32_t k = 0; k < c; k += LB_GROUP_CHUNK) {
+    for (uint32_t k = 0; k < c; k += chunk) {
       chunk_beg[oc] = om + k;
-      chunk_end[oc] = om + min(k + LB_GROUP_CHUNK, c);
+      chunk_end[oc] = om + min(k + chunk, c);
       oc++;
     }
     om += c;
@@ -1924,6 +1927,27 @@ __global__ void __launch_bounds__(LB_TPB) k_job_status(uint32_t n_jobs, const ui
   const int st = job_status_of(a, e, sig_status, pk_status);
   job_status[j] = st;
   for (uint32_t i = a; i < e; i++) set_live[i] = st == LB_OK ? 1u : 0u;
+}
+
+// Speculative liveness for the per-root sums: set_spec[i] = 1 iff set i's job would be live if
+// every signature decodes (the pubkey statuses alone), so the per-root chain needs only the
+// pubkey side, not the signature decode.  A decode failure can only clear a set's liveness:
+// k_live_mismatch flags any set counted in the sums that the full statuses exclude.
+__global__ void __launch_bounds__(LB_TPB) k_spec_live(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
+                                                      const int32_t* __restrict__ pk_status,
+                                                      uint32_t* __restrict__ set_spec) {
+  const uint32_t j = lb_tid();
+  if (j >= n_jobs) return;
+  const uint32_t a = job_off[j], e = job_off[j + 1];
+  bool live = a != e;
+  for (uint32_t i = a; i < e; i++) live &= pk_status[i] == LB_OK;
+  for (uint32_t i = a; i < e; i++) set_spec[i] = live ? 1u : 0u;
+}
+__global__ void __launch_bounds__(LB_TPB) k_live_mismatch(uint32_t n, const uint32_t* __restrict__ set_live,
+                                                          const uint32_t* __restrict__ set_spec,
+                                                          uint32_t* __restrict__ flag) {
+  const uint32_t i = lb_tid();
+  if (i < n && set_spec[i] && !set_live[i]) *flag = 1u;
 }
 
 // chunk c of a group: Jacobian sum of r_i PK_i over its live members -> gacc (stride n)

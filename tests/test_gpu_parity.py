@@ -643,3 +643,24 @@ def test_per_root_kernel_forms_agree(monkeypatch, name):
         assert np.array_equal(got, wl.expected), (lim, np.nonzero(got != wl.expected))
         outs.append(part)
     assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4] == outs[5]
+
+
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_speculative_per_root_chain(monkeypatch, spec):
+    """The per-root sums and Miller loops start on speculative liveness (pubkey statuses only,
+    LB_SPEC_GSUM=1) and are redone with the full statuses when a signature fails to decode.  c4
+    plants malformed signatures in jobs whose roots are shared with valid sets (the sync-committee
+    root): verdicts must equal the planted expectation either way; a valid c2 block too."""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    monkeypatch.setenv("LB_SPEC_GSUM", spec)
+    with Engine(0) as e:
+        for name in ("c4", "c2"):
+            wl = W.make(e, name)
+            b = e.upload(W.indexed_for(e, wl))
+            try:
+                assert np.array_equal(np.asarray(b.verify()), wl.expected), name
+                _, st = b.partial()
+                assert np.array_equal(b.search_after_partial(), wl.expected), name
+            finally:
+                b.free()

@@ -17,5 +17,5 @@ for r in $RUNS; do
   tag=$(echo "$r" | tr ':=/@+' '_____')
   if [ -n "$LEGS" ]; then legs="--legs $LEGS"; else legs="--no-extra"; fi
   env LB_MAX_ENGINES_PER_DEVICE=16 $envs timeout -k 10 300 python3 -u bench.py --inflight $inf --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline $legs > $OUT/$tag.log 2>&1 || { tail -5 $OUT/$tag.log; exit 1; }
-  echo "== $r"; tail -1 $OUT/$tag.log | python3 tools/bench_summary.py | head -3
+  echo "== $r"; tail -1 $OUT/$tag.log | python3 tools/bench_summary.py
 done
