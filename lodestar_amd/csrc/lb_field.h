@@ -432,12 +432,39 @@ LB_HD fp28 lb_tab8_28(const fp28* t, uint32_t k) {
     default: return t[7];
   }
 }
+#ifndef LB_POW28_WIN
+#define LB_POW28_WIN 3  // sliding-window width of the 28-bit-limb chains: 3 keeps the 4 odd powers in
+                        // registers; 4 (8 powers, 448 B per lane) put the table on the stack
+#endif
+template <int NT>
+LB_HD fp28 lb_tab_sel28(const fp28* t, uint32_t k) {  // t[k] by selects (k is wave-uniform)
+  fp28 r = t[0];
+  LB_UNROLL for (int c = 1; c < NT; c++) {
+    const bool s = k == (uint32_t)c;
+    LB_UNROLL for (int w = 0; w < 14; w++) r.l[w] = s ? t[c].l[w] : r.l[w];
+  }
+  return r;
+}
 LB_HD fp fp_pow_const_28(const fp& a, const uint32_t* e, int top_bit) {
-  fp28 tab[8];
+  constexpr int WIN = LB_POW28_WIN, NT = 1 << (WIN - 1);
+  fp28 tab[NT];
   tab[0].l[0] = (a.v[0] << 8) & 0x0fffffffu;  // the limbs of a * 2^8: a's value in R'-form
   LB_UNROLL for (int k = 1; k < 14; k++) tab[0].l[k] = lb_bits28(a.v, 28 * k - 8);
   const fp28 a2 = fp28_sqr(tab[0]);
-  LB_UNROLL for (int k = 1; k < 8; k++) tab[k] = fp28_mul(tab[k - 1], a2);
+  // odd powers one statement each: a loop here stays rolled (its body is too large for the
+  // unroller's budget) and then indexes the table dynamically, i.e. on the stack
+  tab[1] = fp28_mul(tab[0], a2);
+  if constexpr (NT >= 4) {
+    tab[2] = fp28_mul(tab[1], a2);
+    tab[3] = fp28_mul(tab[2], a2);
+  }
+  if constexpr (NT == 8) {
+    tab[4] = fp28_mul(tab[3], a2);
+    tab[5] = fp28_mul(tab[4], a2);
+    tab[6] = fp28_mul(tab[5], a2);
+    tab[7] = fp28_mul(tab[6], a2);
+  }
+  static_assert(NT == 2 || NT == 4 || NT == 8, "window of 2, 3 or 4 bits");
   auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
   fp28 r = tab[0];
   bool first = true;
@@ -448,16 +475,16 @@ LB_HD fp fp_pow_const_28(const fp& a, const uint32_t* e, int top_bit) {
       i--;
       continue;
     }
-    int j = i - 3 > 0 ? i - 3 : 0;
+    int j = i - (WIN - 1) > 0 ? i - (WIN - 1) : 0;
     while (!bit(j)) j++;
     uint32_t val = 0;
     for (int k = i; k >= j; k--) val = (val << 1) | bit(k);
     if (first) {
-      r = lb_tab8_28(tab, val >> 1);
+      r = NT == 8 ? lb_tab8_28(tab, val >> 1) : lb_tab_sel28<NT>(tab, val >> 1);
       first = false;
     } else {
       for (int k = i; k >= j; k--) r = fp28_sqr(r);
-      r = fp28_mul(r, lb_tab8_28(tab, val >> 1));
+      r = fp28_mul(r, NT == 8 ? lb_tab8_28(tab, val >> 1) : lb_tab_sel28<NT>(tab, val >> 1));
     }
     i = j - 1;
   }
@@ -672,6 +699,21 @@ LB_HD bool fp_plain_from_be48(fp& out, const uint8_t* b, uint8_t first_byte_mask
     if (i == 11) b0 &= first_byte_mask;
     out.v[i] = (b0 << 24) | ((uint32_t)b[o + 1] << 16) | ((uint32_t)b[o + 2] << 8) | b[o + 3];
   }
+  const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
+  uint32_t br = 0;
+  LB_UNROLL for (int j = 0; j < 12; j++) {
+    uint64_t d = (uint64_t)out.v[j] - Pl[j] - br;
+    br = (uint32_t)(d >> 63);
+  }
+  return br != 0;  // out < p
+}
+
+// the same from 12 little-endian-loaded words of the 48 bytes (w[k] = bytes 4k..4k+3): no byte
+// buffer, so a kernel keeps the encoding in registers
+LB_HD uint32_t lb_bswap32(uint32_t x) { return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24); }
+LB_HD bool fp_plain_from_be48_w(fp& out, const uint32_t* w, uint8_t first_byte_mask) {
+  LB_UNROLL for (int i = 0; i < 12; i++) out.v[i] = lb_bswap32(w[11 - i]);
+  out.v[11] &= ((uint32_t)first_byte_mask << 24) | 0x00ffffffu;
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
   uint32_t br = 0;
   LB_UNROLL for (int j = 0; j < 12; j++) {

@@ -207,9 +207,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decompress_sigs(uint32_
     a.x = fp2_zero();
     a.y = fp2_zero();
   } else {
-    uint8_t b[96];
-    ld_bytes<96>(b, sigs + (size_t)96 * i);
-    st = g2_decompress96(b, a, inf);
+    uint32_t w[24];
+    const uint4* s = reinterpret_cast<const uint4*>(sigs + (size_t)96 * i);
+    LB_UNROLL for (int k = 0; k < 6; k++) {
+      const uint4 v = s[k];
+      w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+    }
+    st = g2_decompress96_w(w, a, inf);
   }
   soa_st(sig_aff, n, i, a);
   // array-of-structures copy (192 B per set) for the MSM's gathers: one point = 12 x 16 B
@@ -225,29 +229,69 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n
   uint32_t i = lb_tid();
   if (i >= n) return;
   if (sig_status[i] != LB_OK || sig_inf[i]) return;
-  // Scott's test psi(P) == [x]P with [|x|]P by the register-lean ladder (lb_curve.h); P is
-  // re-read from memory at the five additions rather than held across the doublings
-  const volatile uint32_t* vp = sig_aff;
-  auto load_p = [&]() {
-    g2a a;
+  // Scott's test psi(P) == [x]P with [|x|]P by the register-lean ladder (lb_curve.h).  P is
+  // re-read from memory coordinate by coordinate where the additions use it, through a base
+  // pointer re-derived at each read: otherwise the compiler hoists the 48 row addresses (96
+  // VGPRs) out of the ladder and spills them (696 B of private segment per lane before)
+  auto load_f2 = [&](int o) {
+    const uint32_t* base = sig_aff;
+    asm volatile("" : "+s"(base));
+    fp2 a;
     uint32_t* w = reinterpret_cast<uint32_t*>(&a);
-    LB_UNROLL for (int k = 0; k < 48; k++) w[k] = vp[(size_t)k * n + i];
+    LB_UNROLL for (int k = 0; k < 24; k++) w[k] = __builtin_nontemporal_load(base + (size_t)(k + o) * n + i);
     return a;
   };
-  g2j acc = jac_from_aff(load_p());
+  g2j acc = jac_from_aff(g2a{load_f2(0), load_f2(24)});
+  // the exceptional additions (acc == +-P: points of small order outside G2) reuse the loop's one
+  // doubling: acc = P, and the next pass's doubling yields acc + P = 2P for the same bit (redo)
+  bool redo = false;
 #pragma clang loop unroll(disable)
-  for (int b = 62; b >= 0; b--) {
+  for (int b = 62; b >= 0;) {
     g2_dbl_lean<LB_SUBGROUP_INL>(acc);
-    if ((LB_X_ABS >> b) & 1ull) g2_add_aff_lean<LB_SUBGROUP_INL>(acc, load_p());
+    if (redo) {
+      redo = false;
+      b--;
+      continue;
+    }
+    if ((LB_X_ABS >> b) & 1ull) {
+      if (jac_is_inf(acc)) {
+        acc = jac_from_aff(g2a{load_f2(0), load_f2(24)});
+        b--;
+        continue;
+      }
+      // acc + P (madd-2007-bl with Z3 = 2 Z1 H), ordered so Z1Z1 dies before the Karatsuba temporaries
+      const fp2 Z1Z1 = lean2_sqr<LB_SUBGROUP_INL>(acc.z);
+      const fp2 H = fp2_sub(lean2_mul<LB_SUBGROUP_INL>(load_f2(0), Z1Z1), acc.x);
+      const fp2 t = lean2_mul<LB_SUBGROUP_INL>(acc.z, Z1Z1);
+      const fp2 rr = fp2_dbl(fp2_sub(lean2_mul<LB_SUBGROUP_INL>(load_f2(24), t), acc.y));
+      if (fp2_is_zero(H)) {
+        if (fp2_is_zero(rr)) {  // acc == P
+          acc = jac_from_aff(g2a{load_f2(0), load_f2(24)});
+          redo = true;
+        } else {  // acc == -P
+          acc = jac_infinity<fp2>();
+          b--;
+        }
+        continue;
+      }
+      acc.z = fp2_dbl(lean2_mul<LB_SUBGROUP_INL>(acc.z, H));
+      const fp2 I = fp2_mul4(lean2_sqr<LB_SUBGROUP_INL>(H));
+      const fp2 J = lean2_mul<LB_SUBGROUP_INL>(H, I);
+      const fp2 V = lean2_mul<LB_SUBGROUP_INL>(acc.x, I);
+      const fp2 YJ = fp2_dbl(lean2_mul<LB_SUBGROUP_INL>(acc.y, J));
+      acc.x = fp2_sub(fp2_sub(lean2_sqr<LB_SUBGROUP_INL>(rr), J), fp2_dbl(V));
+      acc.y = fp2_sub(lean2_mul<LB_SUBGROUP_INL>(rr, fp2_sub(V, acc.x)), YJ);
+    }
+    b--;
   }
   bool ok = !jac_is_inf(acc);  // psi(P) is finite
   if (ok) {
-    const g2a a = load_p();
-    const fp2 z2 = fp2_sqr(acc.z);
-    ok = fp2_eq(fp2_mul(fp2_mul(fp2_conj(a.x), fp2_load(LB_PSI_CX)), z2), acc.x);
+    const fp2 z2 = lean2_sqr<LB_SUBGROUP_INL>(acc.z);
+    ok = fp2_eq(lean2_mul<LB_SUBGROUP_INL>(lean2_mul<LB_SUBGROUP_INL>(fp2_conj(load_f2(0)), fp2_load(LB_PSI_CX)), z2),
+                acc.x);
     if (ok) {
-      const fp2 py = fp2_mul(fp2_conj(a.y), fp2_load(LB_PSI_CY));
-      ok = fp2_eq(fp2_mul(fp2_mul(py, z2), acc.z), fp2_neg(acc.y));
+      const fp2 py = lean2_mul<LB_SUBGROUP_INL>(fp2_conj(load_f2(24)), fp2_load(LB_PSI_CY));
+      ok = fp2_eq(lean2_mul<LB_SUBGROUP_INL>(lean2_mul<LB_SUBGROUP_INL>(py, z2), acc.z), fp2_neg(acc.y));
     }
   }
   if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;

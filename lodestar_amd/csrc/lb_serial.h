@@ -7,14 +7,15 @@
 #pragma once
 #include "lb_curve.h"
 
-// 96-byte compressed G2 -> affine point (no subgroup check).  inf = point at infinity.
-LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
+// 96-byte compressed G2, as 24 little-endian-loaded words (w[k] = bytes 4k..4k+3) -> affine point
+// (no subgroup check).  inf = point at infinity.
+LB_HD int g2_decompress96_w(const uint32_t* w, g2a& out, bool& inf) {
   inf = false;
-  uint8_t f = b[0];
+  const uint32_t f = w[0] & 0xffu;
   if (!(f & 0x80)) return LB_BAD_ENCODING;
   if (f & 0x40) {
-    uint32_t acc = f & 0x3f;
-    for (int i = 1; i < 96; i++) acc |= b[i];
+    uint32_t acc = w[0] & 0xffffff3fu;
+    for (int i = 1; i < 24; i++) acc |= w[i];
     if (acc) return LB_BAD_ENCODING;
     inf = true;
     out.x = fp2_zero();
@@ -22,8 +23,8 @@ LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
     return LB_OK;
   }
   fp x1, x0;
-  bool ok1 = fp_plain_from_be48(x1, b, 0x1f);
-  bool ok0 = fp_plain_from_be48(x0, b + 48, 0xff);
+  bool ok1 = fp_plain_from_be48_w(x1, w, 0x1f);
+  bool ok0 = fp_plain_from_be48_w(x0, w + 12, 0xff);
   if (!ok0 || !ok1) return LB_BAD_ENCODING;
   fp2 x{fp_to_mont(x0), fp_to_mont(x1)};
   fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), fp2_load(LB_B2));
@@ -34,6 +35,12 @@ LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
   out.x = x;
   out.y = y;
   return LB_OK;
+}
+LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
+  uint32_t w[24];
+  LB_UNROLL for (int k = 0; k < 24; k++)
+    w[k] = (uint32_t)b[4 * k] | ((uint32_t)b[4 * k + 1] << 8) | ((uint32_t)b[4 * k + 2] << 16) | ((uint32_t)b[4 * k + 3] << 24);
+  return g2_decompress96_w(w, out, inf);
 }
 
 // 192-byte uncompressed G2 (x.c1 || x.c0 || y.c1 || y.c0) -> affine point, curve-checked

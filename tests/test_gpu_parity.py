@@ -496,6 +496,43 @@ def test_indexed_null_indices_only_without_keys(engine):
     assert st == N.LB_OK and out[0] == -N.LB_EMPTY_AGGREGATE_ARRAY
 
 
+H2 = 0x5D543A95414E7F1091D50792876A202CD91DE4547085ABAA68A205B2E5A7DDFA628F1CB4D9E82EF21537E293A6691AE1616EC6E786F0C70CF1C38E31C7238E5
+
+
+def small_order_signatures():
+    """Signatures on E'(Fp2) of orders 13 and 23 (torsion of the cofactor h2 = 13^2 23^2 ...): the
+    psi ladder's prefix at bit 60 is 12 = -1 mod 13, so an order-13 point meets acc == -P at an
+    addition (the lane kernel's exceptional branch, then the addition to infinity)."""
+    import oracle.bls_oracle as o
+    q = o.iso_map(o.map_to_curve_sswu(o.hash_to_field_fp2(bytes(range(32)), 2, o.DST_POP)[0]))
+    assert o.g2_mul(q, H2 * o.R) is None
+    out = []
+    for ell in (13, 23):  # ell^2 divides h2: project onto the ell-primary part, then down to order ell
+        Q = o.g2_mul(q, H2 * o.R // (ell * ell))
+        if Q is not None and o.g2_mul(Q, ell) is not None:
+            Q = o.g2_mul(Q, ell)
+        assert Q is not None and o.g2_mul(Q, ell) is None
+        out.append(o.g2_compress(Q))
+        out.append(o.g2_compress(o.g2_neg(Q)))
+    return out
+
+
+@pytest.mark.parametrize("g8_max", ["0", str(1 << 31)])
+def test_small_order_signatures_not_in_group(monkeypatch, g8_max):
+    """Both subgroup-check kernels (one lane per set: k_sig_subgroup; 8 lanes: k_sig_subgroup_g8)
+    reject points of small order with BLST_POINT_NOT_IN_GROUP, in one batch beside valid sets."""
+    from lodestar_amd import _native as N
+    from lodestar_amd.engine import Engine
+    monkeypatch.setenv("LB_SUBGROUP_G8_MAX", g8_max)
+    cases, jobs = case_jobs()
+    valid = jobs[[c["name"] for c in cases].index("single_valid_0")]
+    pk, root = valid[0].pubkeys, valid[0].signing_root
+    bad = [[SetInput(pk, root, sig)] for sig in small_order_signatures()]
+    with Engine(0) as e:
+        codes = e.verify_jobs(bad + [valid] + bad[:1] + [valid])
+    assert codes == [-N.LB_POINT_NOT_IN_GROUP] * 4 + [1, -N.LB_POINT_NOT_IN_GROUP, 1]
+
+
 def test_search_large_roots_parts_then_sets(engine):
     """Two roots of 750 members: one wrong set in root 0 is named by one weighted test over its
     750 single-set parts (weights up to 750, baby-step / giant-step match); root 1's two wrong sets
