@@ -206,11 +206,11 @@ LB_NI jac<F> jac_mul_u64(aff<F> p, uint64_t k) {
 // draw from 2^64 - 1 distinct blinding values, the set size behind blst's 64-bit randomness.
 // (jac_mul_glv_i is the inline body: k_pk_blind keeps the table in registers.)
 template <class F, bool kInl = false>
-LB_HD jac<F> jac_mul_glv_i(const aff<F>& t1, const aff<F>& t2, const aff<F>& t3, uint64_t w) {
+LB_HD jac<F> jac_mul_2d_i(const aff<F>& t1, const aff<F>& t2, const aff<F>& t3, uint64_t k0, uint64_t k1, int bits) {
   jac<F> acc = jac_infinity<F>();
-  for (int i = 31; i >= 0; i--) {
+  for (int i = bits - 1; i >= 0; i--) {
     acc = jac_dbl_i(acc);
-    const uint32_t d = (uint32_t)((w >> i) & 1u) | ((uint32_t)((w >> (32 + i)) & 1u) << 1);
+    const uint32_t d = (uint32_t)((k0 >> i) & 1u) | ((uint32_t)((k1 >> i) & 1u) << 1);
     aff<F> t;
     t.x = d == 1u ? t1.x : (d == 2u ? t2.x : t3.x);
     t.y = d == 1u ? t1.y : (d == 2u ? t2.y : t3.y);
@@ -218,6 +218,10 @@ LB_HD jac<F> jac_mul_glv_i(const aff<F>& t1, const aff<F>& t2, const aff<F>& t3,
     if (d != 0u) acc = s;
   }
   return acc;
+}
+template <class F, bool kInl = false>
+LB_HD jac<F> jac_mul_glv_i(const aff<F>& t1, const aff<F>& t2, const aff<F>& t3, uint64_t w) {
+  return jac_mul_2d_i<F, kInl>(t1, t2, t3, w & 0xffffffffu, w >> 32, 32);
 }
 template <class F>
 LB_NI jac<F> jac_mul_glv(aff<F> t1, aff<F> t2, aff<F> t3, uint64_t w) {

@@ -162,6 +162,9 @@ struct lb_engine {
   dbuf s_root, rs_idx, s_set;
   bool search_rootsum = true;
   bool search_pre = false;  // later rounds take [w] of the kept per-set terms (LB_SEARCH_PRE)
+  // the small rounds' per-position terms: 0 by load (8 lanes per position while the device runs no
+  // other batch, one lane under load), 1 one lane, 2 eight lanes (LB_SMSM_FORM=lane / g8)
+  int smsm_form = 0;
   // large batches: the first round checks the root tree's top subtrees directly, their S_j from
   // one 4-window bucket MSM over all sets, without look-ahead tests and without the per-root sums
   // (one GLV ladder per set); LB_SEARCH_BLOCKS=0 restores the per-root sums + look-ahead round
@@ -317,6 +320,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_MERGE")) e->search_merge = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
+  if (const char* sf = getenv("LB_SMSM_FORM")) e->smsm_form = !strcmp(sf, "lane") ? 1 : !strcmp(sf, "g8") ? 2 : 0;
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
@@ -1158,6 +1162,12 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       else if (pre)  // the per-set terms r_i sig_i are kept from search_root_sums
         hipLaunchKernelGGL(k_smsm_terms_pre, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
                            e->set_uid.as<uint32_t>(), e->s_set.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
+      else if (e->smsm_form == 1 ||
+               (e->smsm_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1))
+        hipLaunchKernelGGL(k_smsm_terms_lane, dim3(nblk_inv(T)), dim3(LB_INV_TPB), 0, s1, T, cm, ma,
+                           e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                           e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_aff.as<uint32_t>(), n,
+                           e->s_terms.as<uint32_t>());
       else
         hipLaunchKernelGGL(k_smsm_terms_g8, dim3((T + 7) / 8), dim3(64), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
                            e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(),

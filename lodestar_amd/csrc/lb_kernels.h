@@ -1575,6 +1575,47 @@ __global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, sm
   }
   if (g8_q() == 0) soa_st(terms, T, t, r);
 }
+// The same terms one lane per position (the form under load: the 8-lane groups issue several times
+// the instructions of one lane's ladder, and a search round's terms were ~40 % of its work): the
+// affine table (sig, [lambda] sig, sig + [lambda] sig) as in k_sig_blind, then the joint ladder
+// over the two (32 + LB_WT_BITS)-bit weighted halves.
+__global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_smsm_terms_lane(uint32_t T, uint32_t c, smsm_args a,
+                                                                 const uint32_t* __restrict__ members,
+                                                                 const uint32_t* __restrict__ set_uid,
+                                                                 const uint64_t* __restrict__ scalars,
+                                                                 const uint32_t* __restrict__ set_live,
+                                                                 const uint32_t* __restrict__ sig_inf,
+                                                                 const uint32_t* __restrict__ sig_aff, uint32_t n,
+                                                                 uint32_t* __restrict__ terms) {
+  const uint32_t t = blockIdx.x * LB_INV_TPB + threadIdx.x;
+  uint32_t j = 0, i = 0, wt = 0;
+  bool act = false;
+  if (t < T) {
+    smsm_member(a, c, t, members, set_uid, j, i, wt);
+    act = msm_live(i, set_live, sig_inf);
+  }
+  g2a t1{fp2_one(), fp2_one()}, t2 = t1;
+  g2j s = jac_infinity<fp2>();
+  if (act) {
+    t1 = soa_ld<g2a>(sig_aff, n, i);
+    t2 = g2a{fp2_mul_fp(t1.x, fp_load(LB_PSI2_CX)), fp2_neg(fp2_mul_fp(t1.y, fp_load(LB_PSI2_CY)))};
+    s = jac_add_aff_i<fp2, true>(jac_from_aff(t1), t2);  // finite: lambda + 1 != 0 mod r
+  }
+  const fp nz = fp_add(fp_sqr(s.z.c0), fp_sqr(s.z.c1));
+  const bool ok = act && !fp_is_zero(nz);
+  const fp ni = fp_inv_block(ok ? nz : fp_one());
+  if (t >= T) return;
+  g2j r = jac_infinity<fp2>();
+  if (ok) {
+    const fp2 zi{fp_mul(s.z.c0, ni), fp_neg(fp_mul(s.z.c1, ni))};
+    const fp2 zi2 = fp2_sqr(zi);
+    const g2a t3{fp2_mul(s.x, zi2), fp2_mul(fp2_mul(s.y, zi2), zi)};
+    const uint64_t wd = scalars[i];
+    r = jac_as<fp2>(jac_mul_2d_i<fp2i, true>(aff_as<fp2i>(t1), aff_as<fp2i>(t2), aff_as<fp2i>(t3),
+                                            (wd & 0xffffffffu) * wt, (wd >> 32) * wt, 32 + LB_WT_BITS));
+  }
+  soa_st(terms, T, t, r);
+}
 // block b sums positions [blo[b], bhi[b]) (<= 64, one instance) -> part[b] (stride nb); the
 // term of position p is terms[perm ? perm[p] : p] (stride T)
 __global__ void __launch_bounds__(64) k_seg_sum64(const uint32_t* __restrict__ blo, const uint32_t* __restrict__ bhi,

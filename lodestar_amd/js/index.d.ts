@@ -47,7 +47,9 @@ export declare class GpuPublicKey {
 }
 
 export declare class BlsGpuVerifier implements IBlsVerifier {
-  /** engines: batches in flight on the device (default 2), each with its own streams + workspace */
+  /** engines: batches in flight on the device (default 2), each with its own streams + workspace; the
+   *  pool also creates one engine for verifyOnMainThread calls, so it takes engines + 1 of the
+   *  per-device cap (LB_MAX_ENGINES_PER_DEVICE, default 16) */
   /** modules as BlsMultiThreadWorkerPool's: metrics.blsThreadPool.* / metrics.bls.* get the same updates */
   constructor(opts?: {device?: number; engines?: number; blsVerifyAllMultiThread?: boolean},
               modules?: {logger?: {error(msg: string, ctx?: object, e?: Error): void}; metrics?: unknown});

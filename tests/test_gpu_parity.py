@@ -570,7 +570,8 @@ def test_search_c3_invalid_two_slots(engine):
 
 @pytest.mark.parametrize("knobs", ["LB_SEARCH_MERGE=0", "LB_ROOT_SHUFFLE=0", "LB_SEARCH_BLOCKS=0",
                                    "LB_SEARCH_BLOCKS=0+LB_SEARCH_MERGE=0",
-                                   "LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0", "LB_SEARCH_BLOCKS=0+LB_SEARCH_PRE=1"])
+                                   "LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0", "LB_SEARCH_BLOCKS=0+LB_SEARCH_PRE=1",
+                                   "LB_SMSM_FORM=lane", "LB_SMSM_FORM=lane+LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0"])
 def test_search_forms_find_the_same_sets(monkeypatch, knobs):
     """Every selectable form of the invalid-set search (lb_engine.hip: look-ahead tests in a
     separate launch pair; the first round over per-root sums with look-ahead tests instead of
@@ -591,6 +592,35 @@ def test_search_forms_find_the_same_sets(monkeypatch, knobs):
             b.free()
     assert np.array_equal(got, wl.expected), (knobs, np.nonzero(got != wl.expected))
     assert (wl.expected == 0).sum() == 2
+
+
+def test_search_term_forms_trace_the_same_rounds(monkeypatch, capfd):
+    """The small rounds' weighted terms one lane per position (k_smsm_terms_lane, the form under
+    load) and by 8-lane groups (k_smsm_terms_g8) must be the same points: with the roots in input
+    order (LB_ROOT_SHUFFLE=0, one tree shape) the search's rounds, failing nodes and direct checks
+    (LB_SEARCH_TRACE) are identical, since a wrong term makes a weighted test match no power and
+    sends its node to direct checks one round later.  (The weighted-test counts are not compared:
+    the look-ahead tests ride along only while the device runs no other batch.)"""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    monkeypatch.setenv("LB_ROOT_SHUFFLE", "0")
+    monkeypatch.setenv("LB_SEARCH_TRACE", "1")
+    traces = []
+    for form in ("g8", "lane"):
+        monkeypatch.setenv("LB_SMSM_FORM", form)
+        capfd.readouterr()
+        with Engine(0) as e:
+            wl = W.make(e, "c3_invalid", slots=2)
+            b = e.upload(W.indexed_for(e, wl))
+            try:
+                got = np.asarray(b.verify())
+            finally:
+                b.free()
+        assert np.array_equal(got, wl.expected), form
+        err = capfd.readouterr().err
+        # "[lb search] round 1: 1 failing nodes, 109 direct checks, 0 weighted tests: 9.952 ms"
+        traces.append([ln.split(", ")[:2] for ln in err.splitlines() if ln.startswith("[lb search]")])
+    assert traces[0] and traces[0] == traces[1], traces
 
 
 def test_aggregate_signatures_golden(engine):
