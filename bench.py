@@ -196,8 +196,9 @@ def roofline(counts, packed, stage_ms):
     return {"bound": "valu-int", "kernel": "stage " + dom, "achieved": ach, "peak": peak,
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": traffic,
             "traffic_note": "HBM bytes per launch of the stage's kernels from FETCH_SIZE + WRITE_SIZE "
-                            "(profiles/traffic.json, rocprofv3 --pmc at this config); the algorithmic bytes "
-                            "are ~300 B per set (DESIGN.md section 5)",
+                            "(profiles/traffic.json, rocprofv3 --pmc at this config, 7 in flight); the decode "
+                            "stage's algorithmic bytes are ~700 B per set: 96 B read and 2 x 192 B + status "
+                            "written by the decompression, 192 B re-read by the subgroup check (DESIGN.md 5.2)",
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}
 

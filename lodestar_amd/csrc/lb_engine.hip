@@ -607,7 +607,9 @@ static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32
   if (e->msm_g8) {
     hipError_t r = e->wsum.ensure((size_t)n_inst * W * sizeof(g2j));
     if (r != hipSuccess) return r;
-    if (entries >= (uint64_t)4 * chunk * nb)
+    // 8-lane bucket sums only while the device runs no other batch: they issue ~6x the
+    // instructions of one lane per bucket (profiles/r4_r3_valu.txt), which under load is the cost
+    if (entries >= (uint64_t)4 * chunk * nb && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1)
       hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(),
                          bcap, e->bsum.as<uint32_t>(), nb);
     else

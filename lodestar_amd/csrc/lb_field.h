@@ -433,8 +433,11 @@ LB_HD fp28 lb_tab8_28(const fp28* t, uint32_t k) {
   }
 }
 #ifndef LB_POW28_WIN
-#define LB_POW28_WIN 3  // sliding-window width of the 28-bit-limb chains: 3 keeps the 4 odd powers in
-                        // registers; 4 (8 powers, 448 B per lane) put the table on the stack
+#define LB_POW28_WIN 4  // sliding-window width of the 28-bit-limb chains.  4: the 8 odd powers on the
+                        // stack (448 B per lane, ~170 VGPRs: three waves per SIMD in the signature
+                        // decode); 3: the 4 powers in registers, no stack, 222 VGPRs (two waves) and
+                        // ~10 % more decode instructions: 1.5 % lower throughput at 7 in flight
+                        // (profiles/r4_regress_ab.txt), for 268 -> 53 MB of decode traffic per batch
 #endif
 template <int NT>
 LB_HD fp28 lb_tab_sel28(const fp28* t, uint32_t k) {  // t[k] by selects (k is wave-uniform)
@@ -453,16 +456,16 @@ LB_HD fp fp_pow_const_28(const fp& a, const uint32_t* e, int top_bit) {
   const fp28 a2 = fp28_sqr(tab[0]);
   // odd powers one statement each: a loop here stays rolled (its body is too large for the
   // unroller's budget) and then indexes the table dynamically, i.e. on the stack
-  tab[1] = fp28_mul(tab[0], a2);
-  if constexpr (NT >= 4) {
-    tab[2] = fp28_mul(tab[1], a2);
-    tab[3] = fp28_mul(tab[2], a2);
-  }
   if constexpr (NT == 8) {
-    tab[4] = fp28_mul(tab[3], a2);
-    tab[5] = fp28_mul(tab[4], a2);
-    tab[6] = fp28_mul(tab[5], a2);
-    tab[7] = fp28_mul(tab[6], a2);
+    // through a loop the unroller leaves rolled: the table indexed dynamically, on the stack
+    // (448 B per lane, cache-resident), at ~170 VGPRs
+    for (int k = 1; k < 8; k++) tab[k] = fp28_mul(tab[k - 1], a2);
+  } else {
+    tab[1] = fp28_mul(tab[0], a2);
+    if constexpr (NT >= 4) {
+      tab[2] = fp28_mul(tab[1], a2);
+      tab[3] = fp28_mul(tab[2], a2);
+    }
   }
   static_assert(NT == 2 || NT == 4 || NT == 8, "window of 2, 3 or 4 bits");
   auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };

@@ -993,7 +993,9 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
 #define LB_GROUP_CHUNK 32  // members summed per lane in k_gsum_chunks
 #ifndef LB_MSM_CHUNK
+#ifndef LB_MSM_CHUNK
 #define LB_MSM_CHUNK 16  // bucket members summed per lane in k_msm_chunks (the batch MSM's serial chain)
+#endif
 #endif
 __device__ __forceinline__ bool msg_eq(const uint8_t* __restrict__ msgs, uint32_t a, uint32_t b) {
   const uint4* x = reinterpret_cast<const uint4*>(msgs + (size_t)32 * a);
