@@ -99,6 +99,9 @@ struct lb_batch {
   }
 };
 
+#ifndef LB_SEARCH_CHUNK_DEF
+#define LB_SEARCH_CHUNK_DEF 8
+#endif
 struct lb_engine {
   int device = 0;
   hipStream_t stream = nullptr;   // s1
@@ -165,6 +168,10 @@ struct lb_engine {
   // the small rounds' per-position terms: 0 by load (8 lanes per position while the device runs no
   // other batch, one lane under load), 1 one lane, 2 eight lanes (LB_SMSM_FORM=lane / g8)
   int smsm_form = 0;
+  // members per lane in the search rounds' bucket MSM chunks (k_msm_chunks).  Its buckets hold ~8
+  // members (109 instances x 1 024 buckets over ~0.9 M entries), so long chunks leave most lanes
+  // of a wave idle behind the longest one; LB_SEARCH_CHUNK
+  uint32_t search_chunk = LB_SEARCH_CHUNK_DEF;
   // large batches: the first round checks the root tree's top subtrees directly, their S_j from
   // one 4-window bucket MSM over all sets, without look-ahead tests and without the per-root sums
   // (one GLV ladder per set); LB_SEARCH_BLOCKS=0 restores the per-root sums + look-ahead round
@@ -321,6 +328,10 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_SEARCH_ROOTSUM")) e->search_rootsum = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SEARCH_PRE")) e->search_pre = std::atoi(sm) != 0;
   if (const char* sf = getenv("LB_SMSM_FORM")) e->smsm_form = !strcmp(sf, "lane") ? 1 : !strcmp(sf, "g8") ? 2 : 0;
+  if (const char* sc = getenv("LB_SEARCH_CHUNK")) {
+    const uint32_t v = (uint32_t)strtoul(sc, nullptr, 10);
+    if (v >= 1 && v <= 64) e->search_chunk = v;
+  }
   if (const char* sm = getenv("LB_SEARCH_BLOCKS")) e->search_blk = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
@@ -1108,7 +1119,8 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
   const bool w4 = std::all_of(mmode.begin(), mmode.end(), [](uint32_t m) { return m == 0u; });
   const uint32_t nwin = w4 ? (uint32_t)LB_MSM_W : (uint32_t)LB_SMSM_W;
   const uint32_t cm = (uint32_t)mlo.size(), T = mpre.back(), nb = cm * nwin * LB_MSM_B;
-  const uint32_t bcap = (2 * nwin * T) / LB_GROUP_CHUNK + nb;
+  const uint32_t schunk = e->search_chunk;
+  const uint32_t bcap = (2 * nwin * T) / schunk + nb;
   LB_HIP(sx_up(e, SX_KIND, dk, s1));
   LB_HIP(sx_up(e, SX_KEY, dkey, s1));
   LB_HIP(sx_up(e, SX_LO, dlo, s1));
@@ -1202,7 +1214,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
                              e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
                              e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->bcnt.as<uint32_t>());
       }
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, (uint32_t)LB_GROUP_CHUNK, e->bcnt.as<uint32_t>(),
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, schunk, e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
                          e->bchunk_end.as<uint32_t>());
       if (T) {
@@ -1221,7 +1233,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
                          e->bchunk_beg.as<uint32_t>(), e->bchunk_end.as<uint32_t>(), e->bmembers.as<uint32_t>(),
                          e->sig_aos.as<uint4>(), bcap, e->bacc.as<uint32_t>(), nb);
       LB_HIP(msm_reduce(e, s1, bcap, nb, cm, w4 ? LB_MSM_W : LB_SMSM_W, U(SX_S), cm, 0u, (uint64_t)2 * nwin * T,
-                        LB_GROUP_CHUNK));
+                        schunk));
     }
     if (c)
       hipLaunchKernelGGL(k_range_pk, dim3(nblk(c)), dim3(LB_TPB), 0, s1, c, U(SX_KIND), U(SX_LO), U(SX_LEN),

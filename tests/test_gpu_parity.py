@@ -571,7 +571,8 @@ def test_search_c3_invalid_two_slots(engine):
 @pytest.mark.parametrize("knobs", ["LB_SEARCH_MERGE=0", "LB_ROOT_SHUFFLE=0", "LB_SEARCH_BLOCKS=0",
                                    "LB_SEARCH_BLOCKS=0+LB_SEARCH_MERGE=0",
                                    "LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0", "LB_SEARCH_BLOCKS=0+LB_SEARCH_PRE=1",
-                                   "LB_SMSM_FORM=lane", "LB_SMSM_FORM=lane+LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0"])
+                                   "LB_SMSM_FORM=lane", "LB_SMSM_FORM=lane+LB_SEARCH_BLOCKS=0+LB_SEARCH_ROOTSUM=0",
+                                   "LB_SEARCH_CHUNK=32", "LB_SEARCH_CHUNK=1"])
 def test_search_forms_find_the_same_sets(monkeypatch, knobs):
     """Every selectable form of the invalid-set search (lb_engine.hip: look-ahead tests in a
     separate launch pair; the first round over per-root sums with look-ahead tests instead of
