@@ -213,11 +213,35 @@ static int g_engine_count[64];
 #define LB_HASH_ALONE_G8 1  // cofactor clearing by 8-lane groups whenever the device is otherwise idle (0: by root count only)
 #endif
 static std::atomic<int> g_device_busy[64];
+// the last pipeline exit per device (steady-clock ns) and the engine it came from
+static std::atomic<int64_t> g_device_exit_ns[64];
+static std::atomic<const void*> g_device_exit_engine[64];
+static int64_t lb_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 struct busy_scope {
   int dev;
-  explicit busy_scope(int d) : dev(d) { g_device_busy[dev].fetch_add(1, std::memory_order_relaxed); }
-  ~busy_scope() { g_device_busy[dev].fetch_sub(1, std::memory_order_relaxed); }
+  const void* eng;
+  busy_scope(int d, const void* e) : dev(d), eng(e) { g_device_busy[dev].fetch_add(1, std::memory_order_relaxed); }
+  ~busy_scope() {
+    g_device_exit_ns[dev].store(lb_now_ns(), std::memory_order_relaxed);
+    g_device_exit_engine[dev].store(eng, std::memory_order_relaxed);
+    g_device_busy[dev].fetch_sub(1, std::memory_order_relaxed);
+  }
 };
+// The device runs no other batch: none inside the pipeline, and none left it within the last
+// LB_ALONE_GRACE_MS unless it was this engine's own (an in-flight engine's host thread between
+// two batches is still load: at 7 in flight those gaps sent batches to the latency forms, ~2 %
+// of the headline, profiles/r4_regress_ab.txt)
+#ifndef LB_ALONE_GRACE_MS
+#define LB_ALONE_GRACE_MS 20
+#endif
+template <class E>
+static bool device_alone(const E* e) {
+  if (g_device_busy[e->device].load(std::memory_order_relaxed) > 1) return false;
+  if (g_device_exit_engine[e->device].load(std::memory_order_relaxed) == (const void*)e) return true;
+  return lb_now_ns() - g_device_exit_ns[e->device].load(std::memory_order_relaxed) > (int64_t)LB_ALONE_GRACE_MS * 1000000;
+}
 static int max_engines_per_device() {
   const char* v = getenv("LB_MAX_ENGINES_PER_DEVICE");
   int k = v ? atoi(v) : 0;
@@ -620,7 +644,7 @@ static hipError_t msm_reduce(lb_engine* e, hipStream_t st, uint32_t bcap, uint32
     if (r != hipSuccess) return r;
     // 8-lane bucket sums only while the device runs no other batch: they issue ~6x the
     // instructions of one lane per bucket (profiles/r4_r3_valu.txt), which under load is the cost
-    if (entries >= (uint64_t)4 * chunk * nb && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1)
+    if (entries >= (uint64_t)4 * chunk * nb && device_alone(e))
       hipLaunchKernelGGL(k_msm_buckets_g8, dim3(nb), dim3(64), 0, st, e->bch.as<uint32_t>(), e->bacc.as<uint32_t>(),
                          bcap, e->bsum.as<uint32_t>(), nb);
     else
@@ -664,7 +688,7 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
   {
     stage_scope sc(e, ST_MILLER, s1);
     const bool shared = e->miller_form == 1 ||
-                        (e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1);
+                        (e->miller_form == 0 && !device_alone(e));
     if (nuh <= e->miller_wave_max) {
       hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                          e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
@@ -846,7 +870,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       stage_scope sc(e, ST_HASH_FIN, s1);
       // 8 lanes per root when the device runs no other batch (a few hundred waves on 1 024 SIMDs:
       // latency), one lane per root under load (2.5x less work), as for the Miller loops below
-      const bool alone = e->miller_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1;
+      const bool alone = e->miller_form == 0 && device_alone(e);
       if (nuh <= e->hash_g8_max || (LB_HASH_ALONE_G8 && alone))
         hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
                            e->h_aff.as<uint32_t>());
@@ -1177,7 +1201,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
         hipLaunchKernelGGL(k_smsm_terms_pre, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma, e->members.as<uint32_t>(),
                            e->set_uid.as<uint32_t>(), e->s_set.as<uint32_t>(), n, e->s_terms.as<uint32_t>());
       else if (e->smsm_form == 1 ||
-               (e->smsm_form == 0 && g_device_busy[e->device].load(std::memory_order_relaxed) > 1))
+               (e->smsm_form == 0 && !device_alone(e)))
         hipLaunchKernelGGL(k_smsm_terms_lane, dim3(nblk_inv(T)), dim3(LB_INV_TPB), 0, s1, T, cm, ma,
                            e->members.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->scalars.as<uint64_t>(),
                            e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->sig_aff.as<uint32_t>(), n,
@@ -1385,7 +1409,7 @@ static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* o
         break;
       }
     }
-    const bool spec_on = LB_SEARCH_SPEC && g_device_busy[e->device].load(std::memory_order_relaxed) <= 1;
+    const bool spec_on = LB_SEARCH_SPEC && device_alone(e);
     for (size_t a = 0; a < work.size();) {
       // a launch set: whole failing nodes until the MSM instance budget is reached
       std::vector<fnode> Fs;
@@ -1525,7 +1549,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
   uint32_t m = 1, mu = 1;
-  busy_scope busy(e->device);
+  busy_scope busy(e->device, e);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   // root verdict on s1 (after the join)
@@ -1572,7 +1596,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
     fp12_to_be576(out576, fp12_one());
     return LB_OK;
   }
-  busy_scope busy(e->device);
+  busy_scope busy(e->device, e);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
@@ -1600,7 +1624,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   if (b->n_jobs == 0) return LB_OK;
   if (e->partial_batch != b) return LB_ERR_ARGUMENT;  // another call ran on this engine since
   LB_HIP(hipSetDevice(e->device));
-  busy_scope busy(e->device);
+  busy_scope busy(e->device, e);
   const uint32_t mu = e->partial_mu, nj = b->n_jobs;
   LB_HIP(e->verdict.ensure(4));
   LB_HIP(e->y_root.ensure(576));
