@@ -203,7 +203,7 @@ struct lb_engine {
 // HIP streams than the device can back with queues and scratch (exhaustion aborts the HSA queue
 // asynchronously instead of returning an error).  LB_MAX_ENGINES_PER_DEVICE overrides the cap.
 // Round 4: 16 (was 7).  Every queue's scratch is reserved for the largest private segment it runs
-// times the device's wave capacity; with the per-root kernels at <= 1.3 KB per lane (k_miller_lane
+// times the device's wave capacity; with the per-root kernels at <= 1.7 KB per lane (k_miller_lane
 // was 6.7 KB) 8 and 10 engines run without an abort (profiles/r4_engines_ab.txt).
 static std::mutex g_engine_mu;
 static int g_engine_count[64];
