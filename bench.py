@@ -37,6 +37,12 @@ Secondary measurements on the same line (rank 0; N = 1 unless noted):
   signing_roots                 getBlockSignatureSets + GPU merkleization from JS (K3 block,
                                 128-attestation block, 32-block segment)
   cpu_baseline / cpu_c1         the reference worker policy on host cores (oracle/cpu_pool.cpp)
+  value_exchange (N > 1)        the headline batches in flight with the single-verdict exchange:
+                                576-byte Fp12 partials all-gathered over RCCL, one final
+                                exponentiation of their product per batch (distributed.py)
+  range_sync_segments (all N)   configs[4]: a 32- and a 64-block segment sharded over the ranks by
+                                cost, partial all-gather + one final exponentiation (strong scaling;
+                                per-rank ms and sets)
 """
 import argparse
 import json
@@ -93,7 +99,7 @@ def parse():
                     help="skip the secondary measurement with every signing root distinct (c3_distinct)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (invalid-set, slots1, latencies, per-config, drop-in)")
-    ap.add_argument("--legs", default="e2e,keys,invalid,slots1,latency,configs,dropin,roots",
+    ap.add_argument("--legs", default="e2e,keys,invalid,slots1,latency,configs,dropin,roots,exchange,segment",
                     help="secondary legs to run (comma list; A/B runs pick one)")
     ap.add_argument("--dropin-engines", type=int, default=4)
     ap.add_argument("--dropin-rounds", type=int, default=10, help="drop-in leg: timed rounds (median reported)")
@@ -185,7 +191,7 @@ def roofline(counts, packed, stage_ms):
     dom = max(per, key=lambda k: per[k]["fp_mul"])
     ach = per[dom]["tmac_s"]
     wall = stage_ms.get("total") or sum(stage_ms.values())
-    traffic = None
+    traffic = traffic_corr = None
     tp = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tp):
         with open(tp) as f:
@@ -193,12 +199,20 @@ def roofline(counts, packed, stage_ms):
         k = t.get("stages", {}).get(dom)
         if k and k.get("sets_per_launch") == packed.n_sets:
             traffic = k["bytes_per_launch"]
+            traffic_corr = k.get("bytes_per_launch_corrected")
+            if traffic_corr is None and t.get("calibration", {}).get("fetch_over_known") and "fetch_bytes" in k:
+                traffic_corr = round(k["fetch_bytes"] / t["calibration"]["fetch_over_known"] + k["write_bytes"])
     return {"bound": "valu-int", "kernel": "stage " + dom, "achieved": ach, "peak": peak,
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": traffic,
-            "traffic_note": "HBM bytes per launch of the stage's kernels from FETCH_SIZE + WRITE_SIZE "
-                            "(profiles/traffic.json, rocprofv3 --pmc at this config, 7 in flight); the decode "
-                            "stage's algorithmic bytes are ~700 B per set: 96 B read and 2 x 192 B + status "
-                            "written by the decompression, 192 B re-read by the subgroup check (DESIGN.md 5.2)",
+            "traffic_corrected": traffic_corr,
+            "traffic_note": "HBM bytes per launch of the stage's kernels (profiles/traffic.json, rocprofv3 --pmc "
+                            "FETCH_SIZE and WRITE_SIZE in separate passes at this config, 7 in flight): `traffic` = "
+                            "raw FETCH_SIZE + WRITE_SIZE; `traffic_corrected` = FETCH_SIZE / the fetch calibration "
+                            "measured on k_msg_insert's known 16 B/lane reads + WRITE_SIZE (MI355X_MICROARCH.md: "
+                            "FETCH_SIZE counts half of a wide read); the decode stage's algorithmic bytes are ~700 B "
+                            "per set: 96 B read and 2 x 192 B + status written by the decompression, 192 B re-read "
+                            "by the subgroup check (DESIGN.md 5.2)",
+            "algorithmic_bytes": 700 * packed.n_sets if dom == "decode_sigs" else None,
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}
 
@@ -445,6 +459,61 @@ def configs_leg(a, eng, W):
     return per
 
 
+def segment_legs(a, eng, W, rank, world, barrier, coll_dev, backend):
+    """configs[4]: a range-sync segment (32 and 64 blocks of ~131 sets, the same segment on every
+    rank) sharded over the ranks by cost (distributed.shard_jobs_by_cost), each rank reducing its
+    shard to a 576-byte Fp12 partial (lb_batch_partial), the partials all-gathered over RCCL and one
+    final exponentiation of their product per rank (distributed.verify_sharded); at N = 1 the
+    partial and the product check run locally.  Strong scaling: the segment is fixed as N grows."""
+    import torch
+    import torch.distributed as dist
+    from lodestar_amd.distributed import shard_jobs_by_cost, verify_sharded
+    out = {}
+    for name, blocks in (("c5", 32), ("c5_64", 64)):
+        wl = W.make(eng, name)
+        lo, hi = shard_jobs_by_cost(wl.packed.job_off, wl.packed.pk_off, world, rank)
+        shard = W.slice_jobs(W.indexed_for(eng, wl), lo, hi)
+        b = eng.upload(shard)
+        try:
+            if world > 1:
+                def step():
+                    return verify_sharded(b.partial, eng.product_is_one, b.search_after_partial,
+                                          device=coll_dev if coll_dev.type == "cuda" else None)
+            else:
+                def step():
+                    f, st = b.partial()
+                    ok = eng.product_is_one([f])
+                    return ([int(x) for x in st] if ok else [int(x) for x in b.search_after_partial()]), ok
+            codes, ok = step()
+            assert ok and np.array_equal(np.asarray(codes), wl.expected[lo:hi]), name
+            reps = max(3, a.steps)
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                codes, ok = step()
+            barrier()
+            el = (time.perf_counter() - t1) / reps
+            assert ok, name
+            mine = torch.tensor([el * 1e3, float(shard.n_sets)], dtype=torch.float64, device=coll_dev)
+            if world > 1:
+                allv = [torch.zeros_like(mine) for _ in range(world)]
+                dist.all_gather(allv, mine)
+                allv = [v.cpu().tolist() for v in allv]
+            else:
+                allv = [mine.cpu().tolist()]
+            ms = max(v[0] for v in allv)
+            out[name] = {"blocks": blocks, "sets": wl.packed.n_sets, "jobs": wl.packed.n_jobs,
+                         "ms_per_segment": round(ms, 3), "sets_per_s": round(wl.packed.n_sets / (ms * 1e-3), 1),
+                         "rank_ms": [round(v[0], 3) for v in allv], "rank_sets": [int(v[1]) for v in allv],
+                         "sharding": "whole jobs, balanced by cost (distributed.shard_jobs_by_cost)",
+                         "exchange": ("all_gather of 576-byte partials (%s) + one final exponentiation" % backend)
+                         if world > 1 else "local partial + one final exponentiation",
+                         "world_size_seen": world}
+        finally:
+            b.free()
+    return out
+
+
 def dropin_leg(a, W, eng_factory):
     """c3 through the JS IBlsVerifier in a node child process (tools/bench_dropin.js)."""
     import shutil
@@ -544,13 +613,14 @@ def main():
 
     # --exchange: every batch in flight has its own process group (created in the same order on
     # every rank), so the engines' all-gathers of different batches proceed independently
+    # (created whenever world > 1: the N > 1 line also carries the exchange leg)
     groups = [None] * a.inflight
-    if a.exchange and world > 1:
+    if world > 1:
         groups = [dist.new_group(list(range(world))) for _ in range(a.inflight)]
 
-    def make_step(k):
+    def make_step(k, exchange=a.exchange):
         b, e = batches[k], engs[k]
-        if not (a.exchange and world > 1):
+        if not (exchange and world > 1):
             return b.verify
         from lodestar_amd.distributed import verify_sharded
 
@@ -595,7 +665,34 @@ def main():
     ms_per_step = el / (a.steps * inflight) * 1e3
     value = n_sets * world * a.steps * inflight / el
 
+    # N > 1: the same batches in flight with the north-star single-verdict exchange (576-byte Fp12
+    # partials all-gathered over RCCL, one final exponentiation of their product per step)
+    exchange_leg = None
+    if world > 1 and not a.exchange and "exchange" in a.legs.split(","):
+        elx = run_inflight(batches, a.steps, wl.expected, barrier,
+                           [make_step(k, exchange=True) for k in range(inflight)])
+        elx_t = torch.tensor([elx], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(elx_t, op=dist.ReduceOp.MAX)
+        elx = float(elx_t.item())
+        exchange_leg = {"value": round(n_sets * world * a.steps * inflight / elx, 1),
+                        "ms_per_step": round(elx / (a.steps * inflight) * 1e3, 3),
+                        "collective": "all_gather of 576-byte Fp12 partials per batch (backend %s)" % backend,
+                        "world_size_seen": world_seen}
     roof = roofline(load_counts(), wl.packed, stage_ms)
+    if roof is not None:
+        # the headline's own fraction: all stages' algorithmic MACs per batch over the measured
+        # time per batch at this configuration (ms_per_step, batches in flight), against the peak
+        cnt = load_counts()
+        work = sum(stage_work(cnt, wl.packed).values()) * cnt["mac_per_fp_mul"]
+        roof["chip_frac"] = round(work / (ms_per_step * 1e-3) / 1e12 / cnt["peak_tmac_s"], 4)
+        roof["chip_frac_note"] = ("sum of every stage's algorithmic Fp-mul x 300 MACs per batch / ms_per_step / "
+                                  "peak: the headline's VALU utilisation, reproducible from this line alone")
+        roof["stage_ms_source"] = ("HIP events on each stage's own stream, one batch in flight, %d profiled steps; "
+                                   "profiles/r5_rocprof_kernel_stats_inflight1.csv holds rocprof's per-kernel "
+                                   "averages for the same configuration" % a.steps)
+    segments = None
+    if a.workload == "c3" and "segment" in a.legs.split(","):
+        segments = segment_legs(a, eng, W, rank, world, barrier, coll_dev, backend)
     # secondary: the same slot shape with every signing root distinct (no sharing to exploit)
     value_distinct = None
     if a.workload == "c3" and not a.no_distinct and not a.exchange:
@@ -664,6 +761,11 @@ def main():
             "batch_latency_ms": round(el / a.steps * 1e3, 1),
             "value_distinct_roots": None if value_distinct is None else round(value_distinct, 1),
         }
+        if exchange_leg is not None:
+            line["value_exchange"] = exchange_leg["value"]
+            line["exchange"] = exchange_leg
+        if segments is not None:
+            line["range_sync_segments"] = segments
         line.update(extra)
         if dropin is not None:
             line["value_dropin"] = dropin.get("value_dropin")

@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "lodestar_amd", "csrc")
@@ -37,17 +38,65 @@ def _deps():
     return hdrs + [os.path.join(INC, "lodestar_bls.h")]
 
 
-def build_lib(force=False, verbose=True):
-    if not force and not _stale(LIB, _deps()):
-        return LIB
-    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-Wno-unused-value", "-I" + INC, "-I" + CSRC,
-           *_sources("lb_engine.hip"), "-o", LIB + ".tmp"]
-    if verbose:
-        print("[build]", " ".join(cmd), flush=True)
+def _jobs():
+    """parallel compiles: the host's CPUs, at most 16 (the GPU box's share), at most one per group"""
+    n = os.cpu_count() or 4
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    return max(1, min(16, n, int(os.environ.get("MAX_JOBS", "16") or 16)))
+
+
+def build_lib(force=False, verbose=True, extra_flags=(), out=None):
+    """The split build (tools/gen_kdecls.py): lb_kgroup.hip once per kernel group (-DLB_KGROUP=g)
+    and lb_engine.hip (host code + launches, -DLB_KGROUP=99), compiled in parallel, linked into
+    one shared library."""
+    out = out or LIB
+    if not force and not extra_flags and not _stale(out, _deps()):
+        return out
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_kdecls
+    cur = open(gen_kdecls.OUT).read() if os.path.exists(gen_kdecls.OUT) else ""
+    if cur != gen_kdecls.render():
+        with open(gen_kdecls.OUT, "w") as f:
+            f.write(gen_kdecls.render())
+    odir = os.path.join(ROOT, "build", "obj" + ("" if out == LIB else "_" + os.path.basename(out)))
+    os.makedirs(odir, exist_ok=True)
+    base = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
+            "-Wno-unused-value", "-I" + INC, "-I" + CSRC, *extra_flags]
+    units = [(os.path.join(CSRC, "lb_engine.hip"), "99", os.path.join(odir, "engine.o"))]
+    units += [(os.path.join(CSRC, "lb_kgroup.hip"), str(g), os.path.join(odir, f"kgroup{g}.o"))
+              for g in range(gen_kdecls.N_GROUPS)]
+    # the slowest units first
+    order = [u for u in units if u[1] in ("3", "6", "8", "9", "7")] + [u for u in units if u[1] not in ("3", "6", "8", "9", "7")]
+    running, failed = [], []
+    t0 = time.time()
+    pend = list(order)
+    while pend or running:
+        while pend and len(running) < _jobs():
+            src, g, obj = pend.pop(0)
+            cmd = base + ["-DLB_KGROUP=" + g, "-c", src, "-o", obj]
+            if verbose:
+                print("[build]", " ".join(cmd[-5:]), flush=True)
+            running.append((subprocess.Popen(cmd), g, time.time()))
+        time.sleep(0.2)
+        for r in list(running):
+            rc = r[0].poll()
+            if rc is not None:
+                running.remove(r)
+                if verbose:
+                    print(f"[build] group {r[1]} done in {time.time() - r[2]:.0f} s (rc {rc})", flush=True)
+                if rc != 0:
+                    failed.append(r[1])
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc (groups {failed})")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *[u[2] for u in units], "-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"[build] {out} in {time.time() - t0:.0f} s", flush=True)
+    return out
 
 
 def build_harness(force=False, verbose=True):

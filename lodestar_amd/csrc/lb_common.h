@@ -5,6 +5,13 @@
 #pragma once
 #include <stdint.h>
 
+// Split build (tools/gen_kdecls.py): a translation unit compiled with -DLB_KGROUP=g defines only
+// the kernels of group g (`#if LB_KG(g)` around each definition); LB_KGROUP unset defines them all
+#ifndef LB_KGROUP
+#define LB_KGROUP -1
+#endif
+#define LB_KG(g) (LB_KGROUP < 0 || LB_KGROUP == (g))
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define LB_HD __host__ __device__ __forceinline__

@@ -22,6 +22,7 @@
 
 #include "lb_kernels.h"
 #include "lb_kzg.h"
+#include "lb_kdecl.h"  // kernels of the other translation units (split build)
 
 #define LB_ABI_VERSION 1
 
@@ -80,6 +81,9 @@ const char* const kStageNames[kStages] = {"decode_sigs", "dedup",   "hash_map", 
 
 struct lb_batch {
   uint32_t n_jobs = 0, n_sets = 0, n_pks = 0;
+  // unique per upload (batch_fill): lb_batch_search_after_partial matches on it, not on the
+  // address, which a freed batch's successor may reuse
+  uint64_t serial = 0;
   std::vector<uint32_t> job_off;  // host copy (bisection bookkeeping)
   std::vector<uint32_t> h_set_chunk_off, h_chunk_lo;  // host staging of the chunk decomposition
   uint32_t n_chunks = 0;           // pubkey aggregation chunks (k_pk_chunks)
@@ -126,9 +130,9 @@ struct lb_engine {
   bool spec_gsum = false;
   dbuf set_spec, live_flag;
   uint32_t* h_flag = nullptr;
-  // the batch whose lb_batch_partial left its state (trees, statuses, scalars) in this engine's
-  // workspace, for lb_batch_search_after_partial; any other pipeline run clears it
-  lb_batch* partial_batch = nullptr;
+  // serial of the batch upload whose lb_batch_partial left its state (trees, statuses, scalars) in
+  // this engine's workspace, for lb_batch_search_after_partial; any other pipeline run clears it
+  uint64_t partial_serial = 0;
   uint32_t partial_mu = 0;
   // bucket sums and the bucket reduction by 8-lane groups (k_msm_buckets_g8, k_msm_window_g8,
   // k_msm_horner_g8); LB_MSM_G8=0: the lone-lane kernels (k_msm_buckets, k_msm_reduce)
@@ -202,20 +206,29 @@ struct lb_engine {
 // Engines per device are capped so that one process cannot create more concurrently active
 // HIP streams than the device can back with queues and scratch (exhaustion aborts the HSA queue
 // asynchronously instead of returning an error).  LB_MAX_ENGINES_PER_DEVICE overrides the cap.
-// Round 4: 16 (was 7).  Every queue's scratch is reserved for the largest private segment it runs
-// times the device's wave capacity; with the per-root kernels at <= 1.7 KB per lane (k_miller_lane
-// was 6.7 KB) 8 and 10 engines run without an abort (profiles/r4_engines_ab.txt).
+// Round 4: 7 -> 10.  Every queue's scratch is reserved for the largest private segment it runs
+// times the device's wave capacity; with the per-root kernels at <= 2.7 KB per lane (k_miller_lane
+// was 6.7 KB) 8 and 10 engines run without an abort (profiles/r4_engines_ab.txt), and
+// lb_engine_create reserves each engine's s1 scratch up front (above).
 static std::mutex g_engine_mu;
 static int g_engine_count[64];
+static std::atomic<uint64_t> g_batch_serial{0};
 // Batches currently inside the pipeline per device (all engines of the process).  With more than
 // one, the device is throughput-bound and the per-root kernels take their work-efficient forms.
 #ifndef LB_HASH_ALONE_G8
 #define LB_HASH_ALONE_G8 1  // cofactor clearing by 8-lane groups whenever the device is otherwise idle (0: by root count only)
 #endif
 static std::atomic<int> g_device_busy[64];
-// the last pipeline exit per device (steady-clock ns) and the engine it came from
-static std::atomic<int64_t> g_device_exit_ns[64];
-static std::atomic<const void*> g_device_exit_engine[64];
+// The two most recent pipeline exits per device by distinct engines (steady-clock ns): exit[0] the
+// latest, exit[1] the latest of any other engine than exit[0]'s, so an engine can ask when ANOTHER
+// engine last left the pipeline (round-4 ADVICE: one slot let an engine that left 1 ms after
+// another see the device as idle while the other was between two batches)
+struct exit_rec {
+  const void* eng = nullptr;
+  int64_t ns = 0;
+};
+static std::mutex g_exit_mu[64];
+static exit_rec g_device_exit[64][2];
 static int64_t lb_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -224,28 +237,37 @@ struct busy_scope {
   const void* eng;
   busy_scope(int d, const void* e) : dev(d), eng(e) { g_device_busy[dev].fetch_add(1, std::memory_order_relaxed); }
   ~busy_scope() {
-    g_device_exit_ns[dev].store(lb_now_ns(), std::memory_order_relaxed);
-    g_device_exit_engine[dev].store(eng, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(g_exit_mu[dev]);
+      exit_rec* r = g_device_exit[dev];
+      if (r[0].eng != eng) r[1] = r[0];
+      r[0] = exit_rec{eng, lb_now_ns()};
+    }
     g_device_busy[dev].fetch_sub(1, std::memory_order_relaxed);
   }
 };
-// The device runs no other batch: none inside the pipeline, and none left it within the last
-// LB_ALONE_GRACE_MS unless it was this engine's own (an in-flight engine's host thread between
-// two batches is still load: at 7 in flight those gaps sent batches to the latency forms, ~2 %
-// of the headline, profiles/r4_regress_ab.txt)
+// The device runs no other batch: none inside the pipeline, and no OTHER engine's batch left it
+// within the last LB_ALONE_GRACE_MS (an in-flight engine's host thread between two batches is
+// still load: at 7 in flight those gaps sent batches to the latency forms, ~2 % of the headline,
+// profiles/r4_regress_ab.txt)
 #ifndef LB_ALONE_GRACE_MS
 #define LB_ALONE_GRACE_MS 20
 #endif
 template <class E>
 static bool device_alone(const E* e) {
   if (g_device_busy[e->device].load(std::memory_order_relaxed) > 1) return false;
-  if (g_device_exit_engine[e->device].load(std::memory_order_relaxed) == (const void*)e) return true;
-  return lb_now_ns() - g_device_exit_ns[e->device].load(std::memory_order_relaxed) > (int64_t)LB_ALONE_GRACE_MS * 1000000;
+  int64_t other;
+  {
+    std::lock_guard<std::mutex> lk(g_exit_mu[e->device]);
+    const exit_rec* r = g_device_exit[e->device];
+    other = r[0].eng != (const void*)e ? r[0].ns : r[1].ns;
+  }
+  return other == 0 || lb_now_ns() - other > (int64_t)LB_ALONE_GRACE_MS * 1000000;
 }
 static int max_engines_per_device() {
   const char* v = getenv("LB_MAX_ENGINES_PER_DEVICE");
   int k = v ? atoi(v) : 0;
-  return k > 0 ? k : 16;
+  return k > 0 ? k : 10;  // the highest engine count measured abort-free (profiles/r4_engines_ab.txt)
 }
 
 #define LB_HIP(call)                                                                        \
@@ -383,6 +405,30 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
   }
+  // Reserve s1's scratch now, one engine at a time, for the largest private segment it can run
+  // (k_miller_lane<2>, 2.7 KB per lane): an empty dispatch over more waves than the device holds.
+  // The runtime sizes a queue's scratch for the largest segment it has run, from one per-process
+  // pool, and a queue that cannot grow it mid-run aborts asynchronously; growing it here, with the
+  // stream synchronised, turns an exhausted pool into LB_ERR_DEVICE from lb_engine_create.
+  {
+    bool ok;
+    {
+      std::lock_guard<std::mutex> lk(g_engine_mu);
+      ok = e->n_u.ensure(4) == hipSuccess && hipMemsetAsync(e->n_u.p, 0, 4, e->stream) == hipSuccess;
+      if (ok) {
+        hipLaunchKernelGGL(k_miller_lane<2>, dim3(4096), dim3(LB_TPB), 0, e->stream, 0u, 1u, e->n_u.as<uint32_t>(),
+                           nullptr, nullptr, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_hash_finish, dim3(4096), dim3(LB_INV_TPB), 0, e->stream, 0u, e->n_u.as<uint32_t>(),
+                           nullptr, nullptr, nullptr, 0u);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(e->stream) == hipSuccess;
+      }
+    }
+    if (!ok) {
+      fprintf(stderr, "lodestar_bls: engine scratch reservation failed on device %d\n", device);
+      lb_engine_destroy(e);
+      return LB_ERR_DEVICE;
+    }
+  }
   *out = e;
   return LB_OK;
 }
@@ -463,6 +509,7 @@ static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint
   if ((n_sets && (!signing_roots || !signatures)) || (n_pks && !pubkeys && !indexed)) return LB_ERR_ARGUMENT;
   LB_HIP(hipSetDevice(e->device));
   b->device = e->device;
+  b->serial = g_batch_serial.fetch_add(1, std::memory_order_relaxed) + 1;
   b->n_jobs = n_jobs;
   b->n_sets = n_sets;
   b->n_pks = n_pks;
@@ -722,7 +769,7 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
 // [0, n_u) live) on s1, joined on s1 ready for the root check.
 static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
-  e->partial_batch = nullptr;
+  e->partial_serial = 0;
   int st = fill_scalars(e, n, scalars);
   if (st != LB_OK) return st;
   mj = 1;
@@ -1613,7 +1660,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   LB_HIP(hipStreamSynchronize(e->stream));
   for (uint32_t j = 0; j < b->n_jobs; j++) out_job[j] = jst[j] == LB_OK ? 1 : -jst[j];
   finish_profile(e);
-  e->partial_batch = b;
+  e->partial_serial = b->serial;
   e->partial_mu = mu;
   return LB_OK;
 }
@@ -1622,7 +1669,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   if (!e || !b || (b->n_jobs && !out_job)) return LB_ERR_ARGUMENT;
   std::lock_guard<std::mutex> lk(e->mu);
   if (b->n_jobs == 0) return LB_OK;
-  if (e->partial_batch != b) return LB_ERR_ARGUMENT;  // another call ran on this engine since
+  if (e->partial_serial == 0 || e->partial_serial != b->serial) return LB_ERR_ARGUMENT;  // another call ran since
   LB_HIP(hipSetDevice(e->device));
   busy_scope busy(e->device, e);
   const uint32_t mu = e->partial_mu, nj = b->n_jobs;
@@ -1644,7 +1691,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   }
   int32_t st = LB_OK;
   if (any_live && !root_ok) st = search_invalid(e, b, mu, out_job);
-  e->partial_batch = nullptr;
+  e->partial_serial = 0;
   return st;
 }
 

@@ -179,6 +179,7 @@ static_assert(LBG_IMAGE % 8 == 0, "lb_group_exec.h: image is a 16-byte multiple"
 // per wave (as k_miller_wave, written into leaf m + u of the product tree).
 // Roots u >= *n_u compute a clamped duplicate and store nothing; a root whose P_u is infinity
 // stores the identity.
+#if LB_KG(5)
 __global__ void __launch_bounds__(64 * LBG_WAVES) k_miller_g8(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
                                                              const uint32_t* __restrict__ gp_aff,
                                                              const uint32_t* __restrict__ gp_inf,
@@ -230,3 +231,4 @@ __global__ void __launch_bounds__(64 * LBG_WAVES) k_miller_g8(uint32_t n, uint32
     LB_UNROLL for (int w = 0; w < 12; w++) treeP[(size_t)(12 * s + w) * (2 * m) + m + u] = v.v[w];
   }
 }
+#endif  // LB_KG

@@ -191,6 +191,7 @@ __device__ __forceinline__ fp fp_inv_block(const fp& z) {
 //   k_decompress_sigs  ZCash decode + Fp2 square root  -> affine point (SoA + AoS), status
 //   k_sig_subgroup     Scott's psi check on the decoded points whose status is still OK
 // sig_status: LB_OK / decode error / LB_POINT_NOT_IN_GROUP / LB_INVALID_SIZE (host-flagged)
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decompress_sigs(uint32_t n, const uint8_t* __restrict__ sigs,
                                                             const uint32_t* __restrict__ sig_sizes,
                                                             uint32_t* __restrict__ sig_aff,
@@ -222,7 +223,9 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_DEC) k_decompress_sigs(uint32_
   sig_inf[i] = inf ? 1u : 0u;
   sig_status[i] = st;
 }
+#endif  // LB_KG
 
+#if LB_KG(1)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                          const uint32_t* __restrict__ sig_inf,
                                                          int32_t* __restrict__ sig_status) {
@@ -296,9 +299,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_SUB) k_sig_subgroup(uint32_t n
   }
   if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
 }
+#endif  // LB_KG
 
 // The same test with 8 lanes per signature (lb_group.h), for small batches (a 1-set call, a
 // block): the |x| ladder's 63 doublings take 3 product levels each instead of 16 serial products.
+#if LB_KG(1)
 __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                         const uint32_t* __restrict__ sig_inf,
                                                         int32_t* __restrict__ sig_status) {
@@ -313,6 +318,7 @@ __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32
   if (ok) ok = jac_eq(g8_psi(g8_unstash(G, 0)), jac_neg(acc));
   if (!ok && g8_q() == 0) sig_status[i] = LB_POINT_NOT_IN_GROUP;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- hash_to_G2
 // ---- expand_message_xmd for a 32-byte message at word level (no byte buffers: the byte-wise
@@ -453,6 +459,7 @@ __device__ __forceinline__ g2j map_to_curve_g2_i(const fp2& u) {
 // Hashing runs once per DISTINCT signing root (k_msg_insert below): launched over 2 nu threads
 // (nu = distinct roots, read back by the host); thread t handles unique message t % nu, field
 // element u_{t / nu}; output Jacobian points q (stride 2n: u_0 of root u at u, u_1 at n + u).
+#if LB_KG(2)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32_t nu,
                                                      const uint32_t* __restrict__ uniq_set,
                                                      const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
@@ -469,6 +476,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32
   }
   soa_st(q, 2 * n, which * n + u, map_to_curve_g2_i(hash_to_field_u(M, (int)which)));
 }
+#endif  // LB_KG
 
 // Lone-lane state parked in an engine-owned global buffer (word w of slot k of root u at
 // st[(k * 72 + w) * n + u]: a wave's lanes touch consecutive words), so long-lived points do not
@@ -577,6 +585,7 @@ __device__ __forceinline__ void g2_add_parked(g2j& p, const uint32_t* st, uint32
 // two [x] ladders over AFFINE bases (the block's batch inversions make them affine: mixed
 // additions, 5 x 14 fewer products per ladder and a smaller live set) and the long-lived points
 // parked (slots: 0 Q, 1 t1 = [x]Q, 2 t3, 3 t1 + psi(Q); 4 x 72 words per lane, stride pn >= grid).
+#if LB_KG(3)
 __global__ void __launch_bounds__(LB_INV_TPB, 1) k_hash_finish(uint32_t n, const uint32_t* __restrict__ n_u,
                                                                   const uint32_t* __restrict__ q,
                                                                   uint32_t* __restrict__ h_aff,
@@ -617,11 +626,13 @@ __global__ void __launch_bounds__(LB_INV_TPB, 1) k_hash_finish(uint32_t n, const
   if (!act) return;
   soa_st(h_aff, n, i, inf2 ? g2a{fp2_zero(), fp2_zero()} : a);
 }
+#endif  // LB_KG
 
 // The same with 8 lanes per root (lb_group.h: each G2 doubling in 3 levels of Fp products, each
 // addition in 6), for batches with few distinct roots, where k_hash_finish's lone-lane
 // cofactor clearing (~2 700 serial Fp products) is the longest step of the per-root chain.
 // Blocks of 64 threads = 8 roots; idle groups of the last block recompute the last root.
+#if LB_KG(8)
 __global__ void __launch_bounds__(64) k_hash_finish_g8(uint32_t n, const uint32_t* __restrict__ n_u,
                                                        const uint32_t* __restrict__ q, uint32_t* __restrict__ h_aff) {
   __shared__ uint32_t g8s[8 * 4 * 72];  // g8_clear_cofactor_st's points, per group
@@ -649,12 +660,14 @@ __global__ void __launch_bounds__(64) k_hash_finish_g8(uint32_t n, const uint32_
   }
   soa_st(h_aff, n, u, a);
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- pubkeys + blinding
 // G1 aggregation (getAggregatedPubkey, utils.ts:5-16) is split into chunks of <= LB_PK_CHUNK
 // keys so a 512-key sync aggregate costs one chunk's latency plus a short combine instead of
 // 512 serial additions on one lane; chunk c covers pubkeys [chunk_lo[c], chunk_lo[c+1]) of one set.
 #define LB_PK_CHUNK 16
+#if LB_KG(4)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                       const uint8_t* __restrict__ pks, uint32_t* __restrict__ chunk_acc,
                                                       int32_t* __restrict__ chunk_status) {
@@ -674,6 +687,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, cons
   soa_st(chunk_acc, nc, c, acc);
   chunk_status[c] = st;
 }
+#endif  // LB_KG
 
 // The resident pubkey table (the epoch cache's index2pubkey, pubkeyCache.ts:56-77): one 128-byte
 // record per key, words 0-23 the affine Montgomery point (g1a), word 24 the flag (decode status
@@ -688,6 +702,7 @@ __device__ __forceinline__ uint32_t table_flag_ld(const uint32_t* __restrict__ t
 }
 
 // Same as k_pk_chunks over the resident pubkey table.  idx = pk_indices.
+#if LB_KG(4)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                           const uint32_t* __restrict__ idx,
                                                           const uint32_t* __restrict__ table, uint32_t table_n,
@@ -715,8 +730,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
   soa_st(chunk_acc, nc, c, jac_as<fp>(acc));
   chunk_status[c] = st;
 }
+#endif  // LB_KG
 
 // decode keys into the resident table (48 B compressed or 96 B uncompressed)
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, const uint8_t* __restrict__ keys,
                                                        uint32_t key_size, int32_t validate, uint32_t first,
                                                        uint32_t* __restrict__ table, int32_t* __restrict__ status) {
@@ -753,9 +770,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_table_fill(uint32_t n, cons
   reinterpret_cast<uint4*>(rec)[6] = tail;
   status[i] = st;
 }
+#endif  // LB_KG
 
 // pk_status: LB_OK / pubkey decode error / LB_EMPTY_AGGREGATE_ARRAY / LB_PK_IS_INFINITY
 // r * PK (Jacobian) for the per-root sums; the affine aggregate PK itself -> pk_aff.  block of LB_INV_TPB threads (fp_inv_block)
+#if LB_KG(4)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
                                                          const uint32_t* __restrict__ chunk_acc,
                                                          const int32_t* __restrict__ chunk_status,
@@ -810,6 +829,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   if (ok) soa_st(pk_aff, n, i, pk);  // the unblinded aggregate, for single-set checks of the search
   pk_status[i] = st;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- Miller loops
 // ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u (bilinearity:
@@ -891,6 +911,7 @@ __device__ __forceinline__ void lane_f_line(const S_t& S, const fp2& l0, const f
 // NL = 3 (f and the temporary in LDS, 54 KB per wave: two waves per CU) keeps the per-root chain
 // fastest; NL = 2 (36 KB: one wave per SIMD, as the registers allow) for batches of so many
 // distinct roots that the LDS bound would leave most of them waiting (lb_engine.hip).
+#if LB_KG(4)
 template <int NL>
 __global__ void __launch_bounds__(LB_TPB, 1) k_miller_lane(uint32_t n, uint32_t m,
                                                            const uint32_t* __restrict__ n_u,
@@ -955,7 +976,9 @@ __global__ void __launch_bounds__(LB_TPB, 1) k_miller_lane(uint32_t n, uint32_t 
   }
 #endif
 }
+#endif  // LB_KG
 
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
                                                     const uint32_t* __restrict__ gp_aff,
                                                     const uint32_t* __restrict__ gp_inf,
@@ -980,6 +1003,7 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
   }
   w_store_soa12(S, LBW_A(0), treeP, 2 * m, m + u);
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- message grouping
 // Sets that sign the same 32-byte root share one hash_to_G2 and one Miller loop (on mainnet a
@@ -1015,6 +1039,7 @@ __device__ __forceinline__ uint32_t msg_hash(const uint8_t* __restrict__ msgs, u
   }
   return (uint32_t)(h >> 32);
 }
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t* __restrict__ msgs, uint64_t key,
                                                        uint32_t cap, uint32_t* __restrict__ tab,
                                                        uint32_t* __restrict__ rep_of) {
@@ -1032,7 +1057,9 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t
   }
   rep_of[i] = rep;
 }
+#endif  // LB_KG
 // Unique-message ids in input order (the first set of each root, LB_ROOT_SHUFFLE=0)
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_uid_input(uint32_t n, const uint32_t* __restrict__ rep_of,
                                                           uint32_t* __restrict__ uid_of,
                                                           uint32_t* __restrict__ uniq_set, uint32_t* __restrict__ n_u) {
@@ -1042,11 +1069,13 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_uid_input(uint32_t n, const uint
   uid_of[i] = u;
   uniq_set[u] = i;
 }
+#endif  // LB_KG
 // Unique-message ids in TABLE-SLOT order (keyed hash: pseudo-random, not the input order): the
 // roots' order is the root product tree's leaf order, and the invalid-set search's first-round
 // subtrees are runs of it.  In input order a run of 64 roots held whole committees of one slot
 // (16 k sets) and the failing subtrees' tests went through the 6-window bucket MSM; shuffled,
 // a subtree holds ~3.5 committee roots on average.
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_uid(uint32_t cap, const uint32_t* __restrict__ tab,
                                                     uint32_t* __restrict__ uid_of, uint32_t* __restrict__ uniq_set,
                                                     uint32_t* __restrict__ n_u) {
@@ -1058,8 +1087,10 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_uid(uint32_t cap, const uint32_t
   uid_of[i] = u;
   uniq_set[u] = i;
 }
+#endif  // LB_KG
 
 // set_uid[i] = unique-message id of set i; pos[i] = its rank inside the group (cnt zeroed)
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t* __restrict__ rep_of,
                                                       const uint32_t* __restrict__ uid_of,
                                                       uint32_t* __restrict__ set_uid, uint32_t* __restrict__ cnt,
@@ -1070,10 +1101,12 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t
   set_uid[i] = u;
   pos[i] = atomicAdd(&cnt[u], 1u);
 }
+#endif  // LB_KG
 
 // One block: exclusive scans of the group sizes (member offsets goff) and of their chunk
 // counts (gch), and the member range of every chunk.  goff[n_u] / gch[n_u] = totals.
 // (n_u == nullptr: nu_const groups; the MSM's buckets use it too)
+#if LB_KG(0)
 __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, uint32_t nu_const, uint32_t chunk,
                                                    const uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ gch,
@@ -1113,7 +1146,9 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     gch[nu] = s_c[1023];
   }
 }
+#endif  // LB_KG
 
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32_t* __restrict__ set_uid,
                                                         const uint32_t* __restrict__ pos,
                                                         const uint32_t* __restrict__ goff,
@@ -1122,6 +1157,7 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32
   if (i >= n) return;
   members[goff[set_uid[i]] + pos[i]] = i;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- sum r_i sig_i by bucket MSM
 // S = sum over live sets of r_i sig_i with r_i = lo_i + hi_i lambda (k_pk_blind): 2n points
@@ -1139,6 +1175,7 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32
 __device__ __forceinline__ bool msm_live(uint32_t i, const uint32_t* set_live, const uint32_t* sig_inf) {
   return set_live[i] && !sig_inf[i];
 }
+#if LB_KG(6)
 __global__ void __launch_bounds__(LB_TPB) k_msm_count(uint32_t n, const uint64_t* __restrict__ scalars,
                                                       const uint32_t* __restrict__ set_live,
                                                       const uint32_t* __restrict__ sig_inf, uint32_t* __restrict__ cnt) {
@@ -1153,6 +1190,8 @@ __global__ void __launch_bounds__(LB_TPB) k_msm_count(uint32_t n, const uint64_t
     }
   }
 }
+#endif  // LB_KG
+#if LB_KG(6)
 __global__ void __launch_bounds__(LB_TPB) k_msm_scatter(uint32_t n, const uint64_t* __restrict__ scalars,
                                                         const uint32_t* __restrict__ set_live,
                                                         const uint32_t* __restrict__ sig_inf,
@@ -1172,8 +1211,10 @@ __global__ void __launch_bounds__(LB_TPB) k_msm_scatter(uint32_t n, const uint64
     }
   }
 }
+#endif  // LB_KG
 // chunk c of a bucket: Jacobian sum of its member points (AoS affine signatures; bit 31 of a
 // member = the [lambda] image).  nb = bucket count (bch has nb + 1 entries).
+#if LB_KG(6)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32_t* __restrict__ bch,
                                                        const uint32_t* __restrict__ chunk_beg,
                                                        const uint32_t* __restrict__ chunk_end,
@@ -1202,7 +1243,9 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_msm_chunks(const uint32
   }
   soa_st(bacc, cap, c, jac_as<fp2>(acc));
 }
+#endif  // LB_KG
 // bucket b = sum of its chunk sums (SoA, stride nb); empty buckets are infinity
+#if LB_KG(6)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t* __restrict__ bch,
                                                         const uint32_t* __restrict__ bacc, uint32_t cap,
                                                         uint32_t* __restrict__ bsum, uint32_t nb) {
@@ -1213,6 +1256,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_msm_buckets(const uint32_t*
     acc = jac_add_i<lb_g2f, true>(acc, jac_as<lb_g2f>(soa_ld<g2j>(bacc, cap, c)));
   soa_st(bsum, nb, b, jac_as<fp2>(acc));
 }
+#endif  // LB_KG
 // One workgroup per MSM instance j of W windows (buckets [j W 256, (j+1) W 256) of bsum, stride
 // nb), one wave per window: lane s owns digits [4 s, 4 s + 4).  A lane's running sums give
 // Y_s = sum_j j B_{4s+j} and T_s = sum_j B_{4s+j} (5 additions); then
@@ -1228,6 +1272,7 @@ __device__ __forceinline__ g2j g2j_shfl_down(const g2j& a, unsigned d) {
              fp2{fp_shfl_down(a.y.c0, d), fp_shfl_down(a.y.c1, d)},
              fp2{fp_shfl_down(a.z.c0, d), fp_shfl_down(a.z.c1, d)}};
 }
+#if LB_KG(6)
 template <int W>
 __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restrict__ bsum, uint32_t nb,
                                                        uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
@@ -1273,6 +1318,7 @@ __global__ void __launch_bounds__(64 * W) k_msm_reduce(const uint32_t* __restric
     soa_st(out, n_out, out0 + blockIdx.x, S);
   }
 }
+#endif  // LB_KG
 
 // ---- the same bucket reduction by 8-lane groups (lb_group.h), for the latency of the chain: a
 // G2 addition is 6 product levels on a group instead of 43 serial products on a lone lane.
@@ -1298,6 +1344,7 @@ __device__ __forceinline__ g2j g2j_shfl(const g2j& a, int src) {
 // bucket b = sum of its chunk sums: one wave per bucket, group g sums chunks g, g + 8, ..., then a
 // 3-level shuffle tree over the groups (as k_msm_buckets, whose lone lane summed ~60 chunk sums
 // serially)
+#if LB_KG(9)
 __global__ void __launch_bounds__(64) k_msm_buckets_g8(const uint32_t* __restrict__ bch,
                                                        const uint32_t* __restrict__ bacc, uint32_t cap,
                                                        uint32_t* __restrict__ bsum, uint32_t nb) {
@@ -1314,12 +1361,14 @@ __global__ void __launch_bounds__(64) k_msm_buckets_g8(const uint32_t* __restric
   }
   if (threadIdx.x == 0) soa_st(bsum, nb, b, acc);
 }
+#endif  // LB_KG
 // Window sums W_w = sum_d d B_d of k_msm_reduce, one workgroup of 4 waves per (instance, window)
 // (one wave per SIMD: a group's G2 addition needs more than 256 registers): group s owns digits
 // [8 s, 8 s + 8) (Y_s = sum_j j B_{8s+j}, T_s = sum_j B_{8s+j}: 13 additions), a 5-level suffix
 // scan U_s = sum_{t >= s} T_t over the 32 groups, V_s = Y_s + 8 U_s (s >= 1), a 5-level tree:
 // sum_d d B_d = sum_s (Y_s + 8 s T_s) = sum_s Y_s + 8 sum_{k >= 1} U_k.
 // wsum: element blockIdx.x = instance * W + w.
+#if LB_KG(9)
 __global__ void __launch_bounds__(256) k_msm_window_g8(const uint32_t* __restrict__ bsum, uint32_t nb,
                                                        uint32_t* __restrict__ wsum, uint32_t n_w) {
   static_assert(LB_MSM_B == 256, "32 groups of 8 digits per window");
@@ -1365,7 +1414,9 @@ __global__ void __launch_bounds__(256) k_msm_window_g8(const uint32_t* __restric
   }
   if (threadIdx.x == 0) soa_st(wsum, n_w, blockIdx.x, v);
 }
+#endif  // LB_KG
 // S_j = sum_w 2^(8 w) W_w (Horner) for instance j = 8 blockIdx.x + group -> out0 + j of `out`
+#if LB_KG(9)
 template <int W>
 __global__ void __launch_bounds__(64) k_msm_horner_g8(const uint32_t* __restrict__ wsum, uint32_t n_inst,
                                                       uint32_t* __restrict__ out, uint32_t n_out, uint32_t out0) {
@@ -1381,11 +1432,13 @@ __global__ void __launch_bounds__(64) k_msm_horner_g8(const uint32_t* __restrict
   }
   if (g8_q() == 0) soa_st(out, n_out, out0 + j, S);
 }
+#endif  // LB_KG
 
 // Small batches: S = sum r_i sig_i without the bucket MSM, whose chunk / bucket / reduction
 // chain is a fixed ~5 ms of serial G2 additions however few the sets.  Each live set's r_i sig_i
 // by 8 lanes (k_sig_blind_g8: GLV double-and-add, [lambda] sig = -psi^2(sig)), then 64:1 shuffle
 // trees (k_g2_sum64) into treeS element 1, where k_msm_reduce would have put it.
+#if LB_KG(9)
 __global__ void __launch_bounds__(64) k_sig_blind_g8(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                      const uint64_t* __restrict__ scalars,
                                                      const uint32_t* __restrict__ set_live,
@@ -1405,11 +1458,13 @@ __global__ void __launch_bounds__(64) k_sig_blind_g8(uint32_t n, const uint32_t*
   }
   if (g8_q() == 0) soa_st(terms, n, i, r);
 }
+#endif  // LB_KG
 // The same terms one lane per set, for mid-size batches (a slot of gossip): 8-lane groups at
 // ~20 k sets fill every SIMD's register file for ~5 ms and stall the per-root kernels of the
 // other stream.  r sig = [lo] sig + [hi] [lambda] sig by jac_mul_glv_i over the affine table
 // (sig, [lambda] sig, sig + [lambda] sig), the third made affine with one batched inversion per
 // block (as k_pk_blind does for G1).
+#if LB_KG(9)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_sig_blind(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                           const uint64_t* __restrict__ scalars,
                                                           const uint32_t* __restrict__ set_live,
@@ -1441,8 +1496,10 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_sig_blind(uint32_t n, c
   }
   soa_st(terms, n, i, r);
 }
+#endif  // LB_KG
 
 // element out0 + b of `out` (stride n_out) = sum of in[64 b .. 64 b + 63] (stride n_in)
+#if LB_KG(9)
 __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* __restrict__ in, uint32_t n_out,
                                                  uint32_t* __restrict__ out, uint32_t out0) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -1454,6 +1511,7 @@ __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* 
   }
   if (threadIdx.x == 0) soa_st(out, n_out, out0 + blockIdx.x, v);
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- invalid-set search
 // After a failing root check the engine searches for the failing sets over NODES: a node is a
@@ -1500,6 +1558,7 @@ __device__ __forceinline__ bool smsm_member(const smsm_args& a, uint32_t c, uint
   wt = md == 0u ? 1u : (md == 1u ? ((set_uid[i] - a.wa[j]) >> a.wb[j]) + 1u : off / a.wa[j] + 1u);
   return true;
 }
+#if LB_KG(7)
 template <int W>
 __global__ void __launch_bounds__(LB_TPB) k_smsm_count(uint32_t T, uint32_t c, smsm_args a,
                                                        const uint32_t* __restrict__ members,
@@ -1522,6 +1581,8 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_count(uint32_t T, uint32_t c, s
     }
   }
 }
+#endif  // LB_KG
+#if LB_KG(7)
 template <int W>
 __global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c, smsm_args a,
                                                          const uint32_t* __restrict__ members,
@@ -1548,11 +1609,13 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_scatter(uint32_t T, uint32_t c,
     }
   }
 }
+#endif  // LB_KG
 // Small search rounds (few thousand positions): the instances' weighted sums without the bucket
 // MSM, whose chunk / bucket / reduction chain is a fixed ~5 ms per round.  Position t's term
 // [w r_i] sig_i = [w lo] sig + [w hi] [lambda] sig (39-bit halves) by 8 lanes, then per-instance
 // sums: blocks of <= 64 positions of one instance (k_seg_sum64), then each instance's block sums
 // (k_seg_final, one wave).
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, smsm_args a,
                                                       const uint32_t* __restrict__ members,
                                                       const uint32_t* __restrict__ set_uid,
@@ -1577,10 +1640,12 @@ __global__ void __launch_bounds__(64) k_smsm_terms_g8(uint32_t T, uint32_t c, sm
   }
   if (g8_q() == 0) soa_st(terms, T, t, r);
 }
+#endif  // LB_KG
 // The same terms one lane per position (the form under load: the 8-lane groups issue several times
 // the instructions of one lane's ladder, and a search round's terms were ~40 % of its work): the
 // affine table (sig, [lambda] sig, sig + [lambda] sig) as in k_sig_blind, then the joint ladder
 // over the two (32 + LB_WT_BITS)-bit weighted halves.
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_smsm_terms_lane(uint32_t T, uint32_t c, smsm_args a,
                                                                  const uint32_t* __restrict__ members,
                                                                  const uint32_t* __restrict__ set_uid,
@@ -1618,8 +1683,10 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_smsm_terms_lane(uint32_
   }
   soa_st(terms, T, t, r);
 }
+#endif  // LB_KG
 // block b sums positions [blo[b], bhi[b]) (<= 64, one instance) -> part[b] (stride nb); the
 // term of position p is terms[perm ? perm[p] : p] (stride T)
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_seg_sum64(const uint32_t* __restrict__ blo, const uint32_t* __restrict__ bhi,
                                                   uint32_t T, const uint32_t* __restrict__ terms, uint32_t nb,
                                                   uint32_t* __restrict__ part, const uint32_t* __restrict__ perm) {
@@ -1632,7 +1699,9 @@ __global__ void __launch_bounds__(64) k_seg_sum64(const uint32_t* __restrict__ b
   }
   if (threadIdx.x == 0) soa_st(part, nb, b, v);
 }
+#endif  // LB_KG
 // instance j = sum of part[bo[j] .. bo[j+1]) -> out element j (stride n_out)
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_seg_final(const uint32_t* __restrict__ bo, const uint32_t* __restrict__ part,
                                                   uint32_t nb, uint32_t* __restrict__ out, uint32_t n_out) {
   const uint32_t j = blockIdx.x;
@@ -1645,12 +1714,14 @@ __global__ void __launch_bounds__(64) k_seg_final(const uint32_t* __restrict__ b
   }
   if (threadIdx.x == 0) soa_st(out, n_out, j, v);
 }
+#endif  // LB_KG
 
 // Root-level search MSM (instances over whole roots: subtrees of the root product tree, modes 0
 // and 1): position t of instance j is root u = rlo_j + (t - pre_j) with weight 1 (mode 0) or
 // ((u - wa_j) >> wb_j) + 1 <= 64 (mode 1), term [w] S_u from the per-root sums S_u = sum r_i sig_i
 // (search_root_sums), one lane per position: 7 doublings + <= 7 additions instead of a 39-bit
 // weighted scalar per SET through the bucket MSM.
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_TPB) k_rsm_terms(uint32_t T, uint32_t c, smsm_args a,
                                                       const uint32_t* __restrict__ s_root, uint32_t nu,
                                                       uint32_t* __restrict__ terms) {
@@ -1667,10 +1738,12 @@ __global__ void __launch_bounds__(LB_TPB) k_rsm_terms(uint32_t T, uint32_t c, sm
   }
   soa_st(terms, T, t, r);
 }
+#endif  // LB_KG
 
 // The set-level instances of a round once the per-set terms T_i = r_i sig_i exist (search_root_sums
 // keeps them): position t's term is [w] T_i, w <= LB_WT_MAX, by an LB_WT_BITS-bit ladder in one lane
 // instead of the 43-bit weighted scalar by 8 lanes (k_smsm_terms_g8).
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_TPB) k_smsm_terms_pre(uint32_t T, uint32_t c, smsm_args a,
                                                            const uint32_t* __restrict__ members,
                                                            const uint32_t* __restrict__ set_uid,
@@ -1688,9 +1761,11 @@ __global__ void __launch_bounds__(LB_TPB) k_smsm_terms_pre(uint32_t T, uint32_t 
   }
   soa_st(terms, T, t, r);
 }
+#endif  // LB_KG
 
 // direct kind-1 nodes: Jacobian sum of r_i PK_i over the part's live members -> pk_out (SoA,
 // stride c)
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, const uint32_t* __restrict__ kind,
                                                        const uint32_t* __restrict__ rlo,
                                                        const uint32_t* __restrict__ rlen,
@@ -1706,11 +1781,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_range_pk(uint32_t c, c
   }
   soa_st(pk_out, c, j, acc);
 }
+#endif  // LB_KG
 // weighted tests over parts of one root (mode 2): sum_k (k + 1) sum_{i in part k} r_i PK_i,
 // one workgroup per test, lane s owning parts k = s + 64 q (f <= LB_WT_MAX, q < 16): with A_q the
 // part sums, sum_q (s + 1 + 64 q) A_q = (s + 1) sum_q A_q + 64 sum_q q A_q, the last by running
 // sums (sum_q q A_q = sum_{j >= 1} sum_{q >= j} A_q): two additions per part and one 7-bit ladder
 // per lane instead of a ladder per part.
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __restrict__ mode,
                                                 const uint32_t* __restrict__ tlo, const uint32_t* __restrict__ tlen,
                                                 const uint32_t* __restrict__ per, const uint32_t* __restrict__ members,
@@ -1750,6 +1827,7 @@ __global__ void __launch_bounds__(64) k_test_pk(uint32_t nt, const uint32_t* __r
   }
   if (lane == 0) soa_st(pk_out, nt, t, sh[0]);
 }
+#endif  // LB_KG
 
 // ML(PK, H_u) of a G1 Jacobian point into area dst (1 for infinity); lane 0 stages the points
 __device__ void w_miller_pk(fp* S, int dst, const g1j& pj_lane0, const uint32_t* __restrict__ h_aff, uint32_t n,
@@ -1845,6 +1923,7 @@ __device__ bool srch_skip(fp* S, const srch_items& I, uint32_t it, const uint32_
   w_load_soa12(S, LBW_A(6), ybuf, I.c + I.nt, I.tyidx[it - I.c]);
   return w_is_one(S, LBW_A(6));
 }
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_search_ml(srch_items I, uint32_t it0, uint32_t cnt, uint32_t cm,
                                                   const uint32_t* __restrict__ treeP, uint32_t n2m,
                                                   const uint32_t* __restrict__ pk_d, const uint32_t* __restrict__ pk_t,
@@ -1912,6 +1991,8 @@ __global__ void __launch_bounds__(64) k_search_ml(srch_items I, uint32_t it0, ui
   }
   w_store_soa12(S, LBW_A(0), ml, N2, 2 * it + side);
 }
+#endif  // LB_KG
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_search_fe(srch_items I, uint32_t it0, uint32_t cnt,
                                                   const uint32_t* __restrict__ ml, uint32_t* __restrict__ ybuf,
                                                   int32_t* __restrict__ verdict) {
@@ -1931,11 +2012,13 @@ __global__ void __launch_bounds__(64) k_search_fe(srch_items I, uint32_t it0, ui
   w_store_soa12(S, LBW_A(0), ybuf, N, it);
   if (threadIdx.x == 0 && it < I.c) verdict[it] = one ? 1 : 0;
 }
+#endif  // LB_KG
 // z = y^k, 1 <= k <= f <= LB_WT_MAX, by baby steps / giant steps: baby[i] = y^(i+1) for i < m
 // (m = min(f, 32), in LDS), then w = z y^(-m j) for j = 0, 1, ... (y^-1 = conj(y): FE values lie
 // in the cyclotomic subgroup) compared by lanes i < m against baby[i] at once; k = m j + i + 1.
 // At most 32 + 32 Fp12 multiplications, against f for the plain walk.
 #define LB_BSGS_M 32
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_search_match(srch_items I, const uint32_t* __restrict__ y_up,
                                                      const uint32_t* __restrict__ ybuf, int32_t* __restrict__ out_k) {
   LBW_SHARED(S);
@@ -1986,6 +2069,7 @@ __global__ void __launch_bounds__(64) k_search_match(srch_items I, const uint32_
   }
   if (threadIdx.x == 0) out_k[t] = hit;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- per-job leaves
 // Job status follows the reference's error precedence: aggregation / pubkey decoding happen
@@ -2003,6 +2087,7 @@ __device__ __forceinline__ int job_status_of(uint32_t a, uint32_t e, const int32
 }
 
 // job_status[j] and, for each of its sets, whether the set takes part in the batch equation
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_job_status(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
                                                        const int32_t* __restrict__ sig_status,
                                                        const int32_t* __restrict__ pk_status,
@@ -2015,11 +2100,13 @@ __global__ void __launch_bounds__(LB_TPB) k_job_status(uint32_t n_jobs, const ui
   job_status[j] = st;
   for (uint32_t i = a; i < e; i++) set_live[i] = st == LB_OK ? 1u : 0u;
 }
+#endif  // LB_KG
 
 // Speculative liveness for the per-root sums: set_spec[i] = 1 iff set i's job would be live if
 // every signature decodes (the pubkey statuses alone), so the per-root chain needs only the
 // pubkey side, not the signature decode.  A decode failure can only clear a set's liveness:
 // k_live_mismatch flags any set counted in the sums that the full statuses exclude.
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_spec_live(uint32_t n_jobs, const uint32_t* __restrict__ job_off,
                                                       const int32_t* __restrict__ pk_status,
                                                       uint32_t* __restrict__ set_spec) {
@@ -2030,14 +2117,18 @@ __global__ void __launch_bounds__(LB_TPB) k_spec_live(uint32_t n_jobs, const uin
   for (uint32_t i = a; i < e; i++) live &= pk_status[i] == LB_OK;
   for (uint32_t i = a; i < e; i++) set_spec[i] = live ? 1u : 0u;
 }
+#endif  // LB_KG
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_live_mismatch(uint32_t n, const uint32_t* __restrict__ set_live,
                                                           const uint32_t* __restrict__ set_spec,
                                                           uint32_t* __restrict__ flag) {
   const uint32_t i = lb_tid();
   if (i < n && set_spec[i] && !set_live[i]) *flag = 1u;
 }
+#endif  // LB_KG
 
 // chunk c of a group: Jacobian sum of r_i PK_i over its live members -> gacc (stride n)
+#if LB_KG(4)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n, const uint32_t* __restrict__ n_u,
                                                         const uint32_t* __restrict__ gch,
                                                         const uint32_t* __restrict__ chunk_beg,
@@ -2056,9 +2147,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
   }
   soa_st(gacc, n, c, jac_as<fp>(acc));
 }
+#endif  // LB_KG
 
 // P_u = sum of the group's chunk sums, to affine (one batched inversion per block); gp_inf[u]
 // flags P_u = infinity (no live member, or members cancelling), whose Miller value is 1.
+#if LB_KG(4)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, const uint32_t* __restrict__ n_u,
                                                            const uint32_t* __restrict__ gch,
                                                            const uint32_t* __restrict__ gacc,
@@ -2086,19 +2179,25 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
   soa_st(gp_aff, n, u, a);
   gp_inf[u] = zero ? 1u : 0u;
 }
+#endif  // LB_KG
 
 // element e of an Fp12 SoA array (stride n) <- 1
+#if LB_KG(0)
 __global__ void __launch_bounds__(64) k_set_one(uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
   if (threadIdx.x == 0) soa_st(base, n, e, fp12_one());
 }
+#endif  // LB_KG
 
 // element e of a G2 Jacobian SoA array (stride n) <- infinity
+#if LB_KG(0)
 __global__ void __launch_bounds__(64) k_g2_set_inf(uint32_t* __restrict__ base, uint32_t n, uint32_t e) {
   if (threadIdx.x == 0) soa_st(base, n, e, jac_infinity<fp2>());
 }
+#endif  // LB_KG
 
 // Message product tree, one level (one wave per node), over leaves [0, *n_u) only.  A node
 // whose leaf range starts at or past *n_u is never read; one whose right half does is a copy.
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const uint32_t* __restrict__ n_u,
                                                   uint32_t* __restrict__ treeP) {
   LBW_SHARED(S);
@@ -2112,9 +2211,11 @@ __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const
   }
   w_store_soa12(S, LBW_A(0), treeP, 2 * m, i);
 }
+#endif  // LB_KG
 
 // fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
 // computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
   LBW_SHARED_ML(S);
   __shared__ int s_inf;
@@ -2141,9 +2242,11 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
     w_miller(S, LBW_A(7));
   w_store_soa12(S, LBW_A(7), fS, 1, 0);
 }
+#endif  // LB_KG
 
 // root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
 // (the FE value y goes to y_out for the invalid-set search)
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
                                                    const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
                                                    uint32_t* __restrict__ y_out) {
@@ -2157,8 +2260,10 @@ __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* _
   w_store_soa12(S, LBW_A(0), y_out, 1, 0);
   if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
+#endif  // LB_KG
 
 // root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
                                                      const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
   LBW_SHARED(S);
@@ -2168,7 +2273,9 @@ __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t*
   w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(w_ld(S, LBW_A(0) + threadIdx.x)));
 }
+#endif  // LB_KG
 
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
                                                        int32_t* __restrict__ ok) {
   LBW_SHARED(S);
@@ -2190,8 +2297,10 @@ __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t
   bool one = w_is_one(S, LBW_A(0));
   if (lane == 0) *ok = (one && !bad) ? 1 : 0;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- pubkey aggregation only
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_aggregate(uint32_t n, const uint32_t* __restrict__ pk_off,
                                                       const uint8_t* __restrict__ pks, uint8_t* __restrict__ out96,
                                                       int32_t* __restrict__ status) {
@@ -2215,12 +2324,14 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_aggregate(uint32_t n, const
   for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
   status[i] = st;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- G2 signature aggregation
 // bls.Signature.aggregate(signatures).toBytes() as the op pools use it for block production
 // (beacon-node/src/chain/opPools/aggregatedAttestationPool.ts:321, attestationPool.ts:184,
 // syncContributionAndProofPool.ts:185): signatures decoded by k_decompress_sigs (+ k_sig_subgroup
 // when validating), summed in chunks of <= LB_PK_CHUNK per lane, then per group.
+#if LB_KG(1)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_sig_agg_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                            const uint32_t* __restrict__ sig_aff, uint32_t n,
                                                            const uint32_t* __restrict__ sig_inf,
@@ -2238,6 +2349,8 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_MSM) k_sig_agg_chunks(uint32_t
   soa_st(chunk_acc, nc, c, acc);
   chunk_status[c] = st;
 }
+#endif  // LB_KG
+#if LB_KG(1)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_agg_groups(uint32_t ng, const uint32_t* __restrict__ group_chunk_off,
                                                            const uint32_t* __restrict__ chunk_acc, uint32_t nc,
                                                            const int32_t* __restrict__ chunk_status,
@@ -2258,11 +2371,13 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sig_agg_groups(uint32_t ng,
   for (int k = 0; k < 96; k++) out96[(size_t)96 * g + k] = ob[k];
   status[g] = st;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- G1 decompression
 // 48-byte compressed pubkeys -> 96-byte uncompressed (the pubkey cache's one-time
 // deserialisation, state-transition/src/cache/pubkeyCache.ts:56-77).  validate = subgroup
 // + infinity check (PublicKey.keyValidate).
+#if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_decompress(uint32_t n, const uint8_t* __restrict__ in48,
                                                           uint8_t* __restrict__ out96, int32_t* __restrict__ status,
                                                           int32_t validate) {
@@ -2288,9 +2403,11 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_decompress(uint32_t n, c
   for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
   status[i] = st;
 }
+#endif  // LB_KG
 
 // ---------------------------------------------------------------- synthetic data (bench/tests)
 // sk (32-byte big-endian, < r) -> 48-byte compressed and 96-byte uncompressed pubkey
+#if LB_KG(2)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks,
                                                      uint8_t* __restrict__ out48, uint8_t* __restrict__ out96) {
   uint32_t i = lb_tid();
@@ -2311,8 +2428,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sk_to_pk(uint32_t n, const 
   if (out96)
     for (int j = 0; j < 96; j++) out96[(size_t)96 * i + j] = u[j];
 }
+#endif  // LB_KG
 
 // sig = sk * H(m), 96-byte compressed
+#if LB_KG(2)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sign(uint32_t n, const uint8_t* __restrict__ sks,
                                                  const uint8_t* __restrict__ msgs, uint8_t* __restrict__ out96) {
   uint32_t i = lb_tid();
@@ -2332,3 +2451,4 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_sign(uint32_t n, const uint
   g2_compress96(c, a, !fin);
   for (int j = 0; j < 96; j++) out96[(size_t)96 * i + j] = c[j];
 }
+#endif  // LB_KG

@@ -23,6 +23,7 @@ __device__ __forceinline__ bool g1_in_subgroup_r(const g1a& a) {
 
 // one point per thread: P_i (table entry i, or 48 compressed bytes) times scalar i (32 bytes,
 // little endian, < r) -> Jacobian SoA terms.  Given points are curve- and subgroup-checked.
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_terms(uint32_t n, const uint8_t* __restrict__ pts48,
                                                      const uint32_t* __restrict__ table, uint32_t table_cap,
                                                      const uint32_t* __restrict__ scalars,
@@ -47,8 +48,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_g1_terms(uint32_t n, const 
   soa_st(terms, n, i, t);
   status[i] = st;
 }
+#endif  // LB_KG
 
 // out[b] = sum of in[64 b .. 64 b + 63] (SoA, strides n_in / n_out), one wave per block
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_g1_sum64(uint32_t n_in, const uint32_t* __restrict__ in, uint32_t n_out,
                                                  uint32_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -60,8 +63,10 @@ __global__ void __launch_bounds__(64) k_g1_sum64(uint32_t n_in, const uint32_t* 
   }
   if (threadIdx.x == 0) soa_st(out, n_out, blockIdx.x, v);
 }
+#endif  // LB_KG
 
 // element 0 of a g1j SoA (stride n) -> 48 compressed bytes
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_g1_out48(const uint32_t* __restrict__ in, uint32_t n, uint8_t* __restrict__ out48) {
   if (threadIdx.x != 0) return;
   const g1j v = soa_ld<g1j>(in, n, 0);
@@ -71,8 +76,10 @@ __global__ void __launch_bounds__(64) k_g1_out48(const uint32_t* __restrict__ in
   g1_compress48(b, a, !fin);
   for (int k = 0; k < 48; k++) out48[k] = b[k];
 }
+#endif  // LB_KG
 
 // decode the trusted setup into the resident tables (G1 points: curve + subgroup checks)
+#if LB_KG(7)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_kzg_setup_g1(uint32_t n, const uint8_t* __restrict__ in48,
                                                          uint32_t* __restrict__ table, uint32_t cap,
                                                          int32_t* __restrict__ status) {
@@ -96,6 +103,8 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_kzg_setup_g1(uint32_t n, co
   soa_st(table, cap, i, a);
   status[i] = st;
 }
+#endif  // LB_KG
+#if LB_KG(7)
 __global__ void __launch_bounds__(64) k_kzg_setup_g2(const uint8_t* __restrict__ in96, uint32_t* __restrict__ g2,
                                                      int32_t* __restrict__ status) {
   const uint32_t i = threadIdx.x;
@@ -110,6 +119,7 @@ __global__ void __launch_bounds__(64) k_kzg_setup_g2(const uint8_t* __restrict__
   for (int k = 0; k < 48; k++) g2[48 * i + k] = w[k];
   status[i] = st;
 }
+#endif  // LB_KG
 
 // verify_kzg_proof_impl: e(C - [y] G1, -G2) e(pi, [tau] G2 - [z] G2) == 1, rewritten with the
 // scalar moved to G1 (bilinearity): e(Q, -G2) e(pi, [tau] G2) == 1 with Q = C - [y] G1 + [z] pi.
@@ -117,6 +127,7 @@ __global__ void __launch_bounds__(64) k_kzg_setup_g2(const uint8_t* __restrict__
 // and pi (c-kzg rejects commitments and proofs outside G1); the two Miller loops and the final
 // exponentiation run on the wave engine.  io[0..47] C, [48..95] pi, scalars y, z (8 LE words
 // each); g2 = [tau^0] G2, [tau^1] G2 (g2a).  *ok = 1 / 0, or -code for a bad point encoding.
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_kzg_check(const uint8_t* __restrict__ io, const uint32_t* __restrict__ yz,
                                                   const uint32_t* __restrict__ g2, int32_t* __restrict__ ok) {
   LBW_SHARED_ML(S);
@@ -198,3 +209,4 @@ __global__ void __launch_bounds__(64) k_kzg_check(const uint8_t* __restrict__ io
   const bool one = w_is_one(S, LBW_A(0));
   if (lane == 0) *ok = one ? 1 : 0;
 }
+#endif  // LB_KG

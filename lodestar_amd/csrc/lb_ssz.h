@@ -56,12 +56,15 @@ LB_HD void ssz_zero_hashes(uint8_t* zh, int n) {
   }
 }
 
+#if LB_KG(2)
 __global__ void __launch_bounds__(64) k_ssz_zero_hashes(uint8_t* __restrict__ zh) {
   if (threadIdx.x == 0) ssz_zero_hashes(zh, 64);
 }
+#endif  // LB_KG
 
 #define LB_SSZ_NO_MIX 0xffffffffffffffffull
 
+#if LB_KG(2)
 __global__ void __launch_bounds__(LB_TPB) k_merkleize(uint32_t n, const uint32_t* __restrict__ chunk_off,
                                                       const uint32_t* __restrict__ depth,
                                                       const uint64_t* __restrict__ mix_len,
@@ -102,3 +105,4 @@ __global__ void __launch_bounds__(LB_TPB) k_merkleize(uint32_t n, const uint32_t
   }
   chunk_st(roots + (size_t)32 * t, root);
 }
+#endif  // LB_KG

@@ -142,11 +142,17 @@ class Batch:
                                                 _p(out, ctypes.c_int32)))
         return bytes(buf), out[: self.n_jobs]
 
-    def search_after_partial(self) -> np.ndarray:
+    def search_after_partial(self, fallback: bool = True) -> np.ndarray:
         """Per-job codes from the state the last partial() of this batch left in the engine (the
-        shard's own root check, then the invalid-set search): lb_batch_search_after_partial."""
+        shard's own root check, then the invalid-set search): lb_batch_search_after_partial.
+        When another call ran on the engine since (LB_ERR_ARGUMENT: the state is gone, e.g. a
+        second thread shares the engine), the shard is re-verified in full (lb_batch_verify), as
+        include/lodestar_bls.h prescribes; fallback=False raises instead."""
         out = np.zeros(max(self.n_jobs, 1), dtype=np.int32)
-        _check(self.engine.lib.lb_batch_search_after_partial(self.engine.h, self.h, _p(out, ctypes.c_int32)))
+        st = self.engine.lib.lb_batch_search_after_partial(self.engine.h, self.h, _p(out, ctypes.c_int32))
+        if st == N.LB_ERR_ARGUMENT and fallback:
+            return self.verify()
+        _check(st)
         return out[: self.n_jobs]
 
     def free(self):

@@ -32,16 +32,20 @@ def _jobs(bad_case=None):
         [cases[n]["expected"] for n in names]
 
 
-def _worker(rank, world, port, bad_case, out):
+def _worker(rank, world, port, bad_case, out, by_cost=False):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
-    from lodestar_amd.distributed import shard_jobs, verify_sharded
+    from lodestar_amd.distributed import shard_jobs, shard_jobs_by_cost, verify_sharded
     from lodestar_amd.engine import pack_jobs
     from oracle.cpu_pool import _lib, run_jobs
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     jobs, _ = _jobs(bad_case)
-    lo, hi = shard_jobs(len(jobs), world, rank)
+    if by_cost:
+        whole = pack_jobs(jobs)
+        lo, hi = shard_jobs_by_cost(whole.job_off, whole.pk_off, world, rank)
+    else:
+        lo, hi = shard_jobs(len(jobs), world, rank)
     packed = pack_jobs(jobs[lo:hi])
     lib = _lib()
     P = lambda a, t: np.ascontiguousarray(a).ctypes.data_as(ctypes.POINTER(t))  # noqa: E731
@@ -67,11 +71,11 @@ def _worker(rank, world, port, bad_case, out):
     dist.destroy_process_group()
 
 
-def _run(bad_case):
+def _run(bad_case, by_cost=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, bad_case, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, bad_case, q, by_cost)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
@@ -97,6 +101,43 @@ def test_gloo_two_ranks_all_valid():
 
 def test_gloo_two_ranks_invalid_job_localised():
     codes, oks = _run("batch_one_wrong")
+    assert oks == [False, False]
+    _, exp = _jobs("batch_one_wrong")
+    assert codes == _expected_codes(exp)
+
+
+def test_shard_jobs_by_cost_balances_unequal_jobs():
+    """whole jobs per rank, balanced by device work (per-set cost + per-key
+    cost), contiguous and covering every job exactly once; a segment of one heavy block job among
+    many 1-set jobs splits by work, not by job count."""
+    from lodestar_amd.distributed import KEY_COST, SET_COST, job_costs, shard_jobs_by_cost
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        n_jobs = int(rng.integers(1, 60))
+        sets = rng.integers(1, 6, n_jobs)
+        job_off = np.concatenate([[0], np.cumsum(sets)])
+        keys = np.where(rng.random(job_off[-1]) < 0.2, rng.integers(100, 512, job_off[-1]), 1)
+        pk_off = np.concatenate([[0], np.cumsum(keys)])
+        cost = job_costs(job_off, pk_off)
+        assert cost.sum() == SET_COST * job_off[-1] + KEY_COST * pk_off[-1]
+        for world in (1, 2, 3, 4, 8):
+            rs = [shard_jobs_by_cost(job_off, pk_off, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n_jobs
+            assert all(rs[r][1] == rs[r + 1][0] and rs[r][0] <= rs[r][1] for r in range(world - 1))
+            # no rank carries more than its share plus one job
+            share = cost.sum() / world
+            for lo, hi in rs:
+                assert cost[lo:hi].sum() <= share + cost.max() + 1
+    # the count-based split would give rank 0 both heavy jobs here; by cost they separate
+    job_off = np.arange(0, 11)
+    pk_off = np.concatenate([[0], np.cumsum([2048, 2048] + [1] * 8)])
+    assert shard_jobs_by_cost(job_off, pk_off, 2, 0) == (0, 1)
+
+
+def test_gloo_two_ranks_cost_sharded_invalid_job_localised():
+    """The exchange protocol over cost-balanced shards (unequal jobs: aggregates of many keys
+    beside single sets) localises the invalid job like the count-based split."""
+    codes, oks = _run("batch_one_wrong", by_cost=True)
     assert oks == [False, False]
     _, exp = _jobs("batch_one_wrong")
     assert codes == _expected_codes(exp)
@@ -179,6 +220,28 @@ def test_search_after_partial_matches_verify():
                 b.partial()
                 b.verify()
                 with pytest.raises(BlsError):
-                    b.search_after_partial()
+                    b.search_after_partial(fallback=False)
+                # the default falls back to a full re-verification of the shard
+                assert np.array_equal(b.search_after_partial(), wl.expected), name
             finally:
                 b.free()
+
+
+@pytest.mark.gpu
+def test_search_after_partial_rejects_a_successor_batch():
+    """partial(b1), free b1, upload b2 (which may reuse b1's address): search_after_partial(b2)
+    must not continue from b1's state (round-4 ADVICE: the check compared raw pointers)."""
+    from lodestar_amd import workloads as W
+    from lodestar_amd.engine import BlsError, Engine
+    with Engine(0) as eng:
+        w4, w2 = W.make(eng, "c4"), W.make(eng, "c2")
+        b1 = eng.upload(W.indexed_for(eng, w4))
+        b1.partial()
+        b1.free()
+        b2 = eng.upload(W.indexed_for(eng, w2))
+        try:
+            with pytest.raises(BlsError):
+                b2.search_after_partial(fallback=False)
+            assert np.array_equal(b2.search_after_partial(), w2.expected)
+        finally:
+            b2.free()

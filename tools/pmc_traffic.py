@@ -3,9 +3,12 @@ batch in flight: per kernel, average (FETCH_SIZE + WRITE_SIZE) x 1024 bytes per 
 pipeline stage (bench.py roofline), the bytes of all the stage's kernel launches per batch
 (batches = launches of k_decompress_sigs, one per batch).
 
-FETCH_SIZE / WRITE_SIZE are in KB (L2 <-> fabric).  MI355X_MICROARCH.md: FETCH_SIZE under-reports
-wide (16 B/lane) streaming reads by 2x; these kernels read 4-byte SoA words and scratch, an
-uncalibrated width, so the raw value is reported.
+FETCH_SIZE / WRITE_SIZE are in KB (L2 <-> fabric).  MI355X_MICROARCH.md: FETCH_SIZE reports half
+the bytes of a wide (16 B/lane) streaming read, other widths are uncalibrated.  The calibration is
+measured here on k_msg_insert, whose reads are known (32-byte roots as 16 B/lane loads + ~4 B of
+table probe per set): `fetch_over_known`.  Each kernel and stage carries the raw bytes
+(FETCH_SIZE + WRITE_SIZE) and the corrected bytes (FETCH_SIZE / fetch_over_known + WRITE_SIZE;
+WRITE_SIZE is exact for the guide's store widths), side by side.
 
   python tools/pmc_traffic.py FETCH.csv WRITE.csv SETS_PER_BATCH > profiles/traffic.json
 """
@@ -55,18 +58,22 @@ def main():
                               "fetch_bytes": round(f), "fetch_over_known": round(f / (32 * n), 3),
                               "note": "MI355X_MICROARCH.md: FETCH_SIZE counts half of a 16 B/lane streaming read; "
                                       "the stage totals below are raw FETCH_SIZE + WRITE_SIZE"}
+    cal = out.get("calibration", {}).get("fetch_over_known") or 1.0
     for k in sorted(set(fetch) & set(write)):
         if not k.startswith("k_"):
             continue
         f, w = fetch[k], write[k]
-        out["kernels"][k] = {"launches": len(f), "fetch_bytes": round(sum(f) / len(f) * 1024),
-                             "write_bytes": round(sum(w) / len(w) * 1024),
-                             "bytes_per_launch": round((sum(f) / len(f) + sum(w) / len(w)) * 1024)}
+        fb, wb = sum(f) / len(f) * 1024, sum(w) / len(w) * 1024
+        out["kernels"][k] = {"launches": len(f), "fetch_bytes": round(fb), "write_bytes": round(wb),
+                             "bytes_per_launch": round(fb + wb), "bytes_per_launch_corrected": round(fb / cal + wb)}
     batches = len(fetch.get("k_decompress_sigs", [])) or 1
     for st, ks in STAGES.items():
-        tot = sum(sum(fetch.get(k, [])) + sum(write.get(k, [])) for k in ks)
-        if tot:
-            out["stages"][st] = {"kernels": [k for k in ks if k in fetch], "bytes_per_launch": round(tot * 1024 / batches),
+        fb = sum(sum(fetch.get(k, [])) for k in ks) * 1024 / batches
+        wb = sum(sum(write.get(k, [])) for k in ks) * 1024 / batches
+        if fb + wb:
+            out["stages"][st] = {"kernels": [k for k in ks if k in fetch], "bytes_per_launch": round(fb + wb),
+                                 "fetch_bytes": round(fb), "write_bytes": round(wb),
+                                 "bytes_per_launch_corrected": round(fb / cal + wb), "fetch_calibration": cal,
                                  "sets_per_launch": n, "batches": batches}
     json.dump(out, sys.stdout, indent=1)
 
