@@ -689,7 +689,8 @@ def main():
                                   "peak: the headline's VALU utilisation, reproducible from this line alone")
         roof["stage_ms_source"] = ("HIP events on each stage's own stream, one batch in flight, %d profiled steps; "
                                    "profiles/r5_rocprof_kernel_stats_inflight1.csv holds rocprof's per-kernel "
-                                   "averages for the same configuration" % a.steps)
+                                   "averages for the same configuration; tools/trace_stage_avg.py -> "
+                                   "profiles/r5_inflight1_decode_check.json compares them" % a.steps)
     segments = None
     if a.workload == "c3" and "segment" in a.legs.split(","):
         segments = segment_legs(a, eng, W, rank, world, barrier, coll_dev, backend)

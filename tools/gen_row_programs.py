@@ -1,0 +1,359 @@
+#!/usr/bin/env python3
+"""Row-engine programs (lodestar_amd/csrc/lb_row.h): the wave programs' formulas re-encoded for
+an engine that runs each Fp product on one 16-lane ROW (lane k holds limb k of 14 signed 28-bit
+limbs, Montgomery radix R' = 2^392) instead of one lane.
+
+Output: lodestar_amd/csrc/lb_row_progs.h (generated; do not edit).
+
+The programs (MUL12, SQR12, FROB, FROB2, DBL_STEP, ADD_STEP; tools/gen_wave_programs.py traces
+them from the tower formulas) keep their slot map and phase schedule; only the encoding changes
+(int32 words, signed coefficients, one record per row task):
+
+  program   [n_phases, n_out, out_slot * n_out]
+  phase     [kind | flags << 8 | n_tasks << 16, nx | ny << 16], then n_tasks records
+  record    kind 0 (product): [dst, x pairs * nx, y pairs * ny]; kind 1 (linear): [dst, pairs * nx]
+  pair      (slot & 0xffff) | (coef << 16), coef a signed 16-bit integer; padding: the zero slot,
+            coefficient 0
+  flags     bit 0: every task's x operand is one slot with coefficient 1 (read as is, no
+            reduction); bit 1: the same for y
+
+Arithmetic (mirrored exactly by RowModel below and checked against big integers and the oracle):
+a slot value v is an integer in (-2p, 2p) congruent to the element times R' (mod p); an operand
+or linear output is the signed limb sum, reduced by a quotient estimate from its top two limbs
+(q = floor((l13 2^28 + l12) 2^336 / p) in double precision) to [0, p) up to an error far below p;
+a product is the row Montgomery product (lb_row.h rp_mul): |x y| / R' + 1.0001 p.
+"""
+import math
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+import gen_wave_programs as G  # noqa: E402
+
+P = G.P
+RP = 1 << 392
+M28 = (1 << 28) - 1
+PINV = (-pow(P, -1, RP)) % RP
+PL = [(P >> (28 * i)) & M28 for i in range(14)]
+PPL = [(PINV >> (28 * i)) & M28 for i in range(14)]
+INV_P336 = (1 << 336) / P
+OUT_PATH = os.path.join(ROOT, "lodestar_amd", "csrc", "lb_row_progs.h")
+N_CONST = G.N_CONST
+
+
+# ------------------------------------------------------------ exact model of lb_row.h
+def val(l):
+    return sum(v << (28 * k) for k, v in enumerate(l[:14]))
+
+
+def limbs(v):
+    """normalized limbs of a signed integer (limbs 0..12 in [0, 2^28), limb 13 signed)"""
+    out = []
+    for _ in range(13):
+        out.append(v & M28)
+        v >>= 28
+    return out + [v, 0, 0]
+
+
+def _shr(v, s):
+    return [0] * s + v[:16 - s]
+
+
+def _shl(v, s):
+    return v[s:] + [0] * s
+
+
+def _i32(x):
+    assert -(1 << 31) <= x < (1 << 31), x
+    return x
+
+
+def norm(v, keep_top):
+    """lb_row.h rp_norm: two carry rounds (64-bit, then 32-bit); keep_top: limb 13 keeps its
+    whole value and takes limb 12's carry whole (the result is a value, not a residue mod 2^392)"""
+    for x in v:
+        assert -(1 << 63) <= x < (1 << 63)
+    q = [x >> 28 for x in v]
+    l = [x & M28 for x in v]
+    qlo = [x & M28 for x in q]
+    qhi = [x >> 28 for x in q]
+    if keep_top:
+        qlo[12], qhi[12] = q[12], 0
+        l[13], qlo[13], qhi[13] = v[13], 0, 0
+        for k in (14, 15):
+            l[k] = qlo[k] = qhi[k] = 0
+    l = [_i32(_i32(a) + b + c) for a, b, c in zip(l, _shr(qlo, 1), _shr(qhi, 2))]
+    c = [x >> 28 for x in l]
+    l2 = [x & M28 for x in l]
+    if keep_top:
+        c[13] = 0
+        l2[13] = l[13]
+    l2 = [_i32(a + b) for a, b in zip(l2, _shr(c, 1))]
+    if keep_top:
+        l2[14] = l2[15] = 0
+    return l2
+
+
+def rp_mul(x, y):
+    y = y[:14] + [0, 0]
+    lo, hi = [0] * 16, [0] * 16
+    for i in range(14):
+        sl = _shr(y, i)
+        sh = _shl(y, 16 - i) if i else [0] * 16
+        lo = [a + x[i] * b for a, b in zip(lo, sl)]
+        hi = [a + x[i] * b for a, b in zip(hi, sh)]
+    t = norm(lo, False)
+    t = [t[k] if k < 14 else 0 for k in range(16)]
+    mc = [0] * 16
+    for i in range(14):
+        mc = [a + PPL[i] * b for a, b in zip(mc, _shr(t, i))]
+    m = norm(mc, False)
+    m = [m[k] if k < 14 else 0 for k in range(16)]
+    for i in range(14):
+        lo = [a + PL[i] * b for a, b in zip(lo, _shr(m, i))]
+        hi = [a + PL[i] * b for a, b in zip(hi, _shl(m, 16 - i) if i else [0] * 16)]
+    for v in lo + hi:
+        assert -(1 << 63) <= v < (1 << 63)
+    E = lo[13] + (lo[12] >> 28) + (lo[11] >> 56)
+    C = (E + M28) >> 28
+    w = [0] * 16
+    w[14], w[15] = lo[14] + C, lo[15]
+    r = [a + b for a, b in zip(_shl(w, 14), _shr(hi, 2))]
+    return norm(r, True)
+
+
+def lin(terms, reduce=True):
+    """signed limb sum of (coef, limbs) terms, then the quotient-estimate reduction"""
+    acc = [0] * 16
+    for c, l in terms:
+        acc = [a + c * x for a, x in zip(acc, l)]
+    if not reduce:
+        return norm(acc, True)
+    w = float(acc[13]) * 268435456.0 + float(acc[12])
+    q = int(math.floor(w * INV_P336))
+    acc = [a - q * (PL[k] if k < 14 else 0) for k, a in enumerate(acc)]
+    return norm(acc, True)
+
+
+def to_row(x):
+    """the R'-form limbs of a field element x (the value x 2^392 mod p, below p)"""
+    return limbs(x * RP % P)
+
+
+def from_row(l):
+    return val(l) * pow(RP, -1, P) % P
+
+
+# ------------------------------------------------------------ encoding
+class RowCode:
+    def __init__(self, words, n_prods, n_lins, n_phases, ntemp):
+        self.words, self.n_prods, self.n_lins, self.n_phases, self.ntemp = words, n_prods, n_lins, n_phases, ntemp
+
+
+ZERO_SLOT = G.CONST_BASE + G.C_ZERO
+
+
+def _pair(slot, coef):
+    assert 0 <= slot < 32768 and -32768 <= coef < 32768
+    return (slot & 0xFFFF) | ((coef & 0xFFFF) << 16)
+
+
+def encode(pg):
+    nst = max([p[0] for p in pg.prods] + [l[0] for l in pg.lins] + [0])
+    phases = []
+    for s in range(nst + 1):
+        pr = [p for p in pg.prods if p[0] == s]
+        if pr:
+            phases.append((0, pr))
+        for v in sorted({l[1] for l in pg.lins if l[0] == s}):
+            phases.append((1, [l for l in pg.lins if l[0] == s and l[1] == v]))
+    out = [len(phases), len(pg.outs)] + list(pg.outs)
+
+    def pairs(lin, width):
+        ps = [_pair(s, c) for s, c in sorted(lin.d.items())]
+        assert len(ps) <= width
+        return ps + [_pair(ZERO_SLOT, 0)] * (width - len(ps))
+
+    def plain(lins):
+        return all(len(l.d) == 1 and list(l.d.values())[0] == 1 for l in lins)
+
+    for kind, tasks in phases:
+        if kind == 0:
+            xs, ys = [t[2] for t in tasks], [t[3] for t in tasks]
+            nx, ny = max(len(x.d) for x in xs), max(len(y.d) for y in ys)
+            flags = (1 if plain(xs) else 0) | (2 if plain(ys) else 0)
+            out += [kind | (flags << 8) | (len(tasks) << 16), nx | (ny << 16)]
+            for t in tasks:
+                out += [t[1]] + pairs(t[2], nx) + pairs(t[3], ny)
+        else:
+            ls = [t[3] for t in tasks]
+            nx = max(len(l.d) for l in ls)
+            out += [kind | (len(tasks) << 16), nx]
+            for t in tasks:
+                out += [t[2]] + pairs(t[3], nx)
+    return RowCode(out, len(pg.prods), len(pg.lins), len(phases), pg.ntemp)
+
+
+def run_row(words, slots):
+    """Interpret a row program over slot -> limbs with exactly lb_row.h's arithmetic."""
+    n_ph, n_out = words[0], words[1]
+    outs = words[2:2 + n_out]
+    pos = 2 + n_out
+    S = dict(slots)
+
+    def operand(ps, is_plain):
+        terms = []
+        for w in ps:
+            slot, coef = w & 0xFFFF, (w >> 16) - ((w >> 16) & 0x8000) * 2
+            terms.append((coef, S[slot]))
+        if is_plain:
+            assert len(terms) == 1 and terms[0][0] == 1
+            return terms[0][1]
+        return lin(terms)
+
+    for _ in range(n_ph):
+        h0, h1 = words[pos], words[pos + 1]
+        pos += 2
+        kind, flags, n = h0 & 0xFF, (h0 >> 8) & 0xFF, h0 >> 16
+        nx, ny = h1 & 0xFFFF, h1 >> 16
+        rs = 1 + nx + (ny if kind == 0 else 0)
+        new = {}
+        for k in range(n):
+            rec = words[pos + k * rs: pos + (k + 1) * rs]
+            if kind == 0:
+                x = operand(rec[1:1 + nx], flags & 1)
+                y = operand(rec[1 + nx:1 + nx + ny], flags & 2)
+                new[rec[0]] = rp_mul(x, y)
+            else:
+                new[rec[0]] = operand(rec[1:1 + nx], False)
+        for v in new.values():
+            assert abs(val(v)) < 2 * P, "slot bound"
+        S.update(new)
+        pos += n * rs
+    return [S[o] for o in outs]
+
+
+def consts_values():
+    """the CONST slots as field elements (same order as lb_wave.h w_init_consts)"""
+    sys.path.insert(0, ROOT)
+    from oracle import bls_oracle as o
+    c = [0] * N_CONST
+    c[G.C_B3], c[G.C_B3 + 1] = 12, 12
+    c[G.C_INV2] = pow(2, P - 2, P)
+    xi = (1, 1)
+    for k in range(1, 6):
+        g = o.f2_pow(xi, k * (P - 1) // 6)
+        c[G.C_FROB1 + 2 * (k - 1)], c[G.C_FROB1 + 2 * (k - 1) + 1] = g
+        c[G.C_FROB2 + k - 1] = o.f2_pow(xi, k * (P * P - 1) // 6)[0]
+    c[G.C_ZERO] = 0
+    return c
+
+
+def _checks(codes):
+    sys.path.insert(0, ROOT)
+    from oracle import bls_oracle as o
+    rnd = random.Random(11)
+    cv = consts_values()
+    base = {G.CONST_BASE + k: to_row(v) for k, v in enumerate(cv)}
+
+    def f12(v):
+        c = [(v[0], v[1]), (v[6], v[7]), (v[2], v[3]), (v[8], v[9]), (v[4], v[5]), (v[10], v[11])]
+        return o.f12_from_f2_coeffs(c)
+
+    for _ in range(2):
+        a = [rnd.randrange(P) for _ in range(12)]
+        b = [rnd.randrange(P) for _ in range(12)]
+        S = dict(base)
+        S.update({G.IN_BASE + k: to_row(a[k]) for k in range(12)})
+        S.update({G.IN_BASE + 12 + k: to_row(b[k]) for k in range(12)})
+        got = [from_row(v) for v in run_row(codes["MUL12"].words, S)]
+        assert f12(got) == o.f12_mul(f12(a), f12(b)), "MUL12"
+        got = [from_row(v) for v in run_row(codes["SQR12"].words, S)]
+        assert f12(got) == o.f12_sqr(f12(a)), "SQR12"
+        got = [from_row(v) for v in run_row(codes["FROB"].words, S)]
+        assert f12(got) == o.f12_pow(f12(a), P), "FROB"
+        got = [from_row(v) for v in run_row(codes["FROB2"].words, S)]
+        assert f12(got) == o.f12_pow(f12(a), P * P), "FROB2"
+    # a few Miller steps against the lone-lane programs' interpreter (values, not limbs)
+    Pp = o.sk_to_pk(0x1234567)
+    Qq = o.hash_to_g2(b"\x07" * 32)
+    f = [rnd.randrange(P) for _ in range(12)]
+    T = [Qq[0][0], Qq[0][1], Qq[1][0], Qq[1][1], 5, 7]
+    for name, vals in (("DBL_STEP", f + T + [Pp[0], Pp[1]]),
+                       ("ADD_STEP", f + T + [Qq[0][0], Qq[0][1], Qq[1][0], Qq[1][1], Pp[0], Pp[1]])):
+        S = dict(base)
+        S.update({G.IN_BASE + k: to_row(v) for k, v in enumerate(vals)})
+        got = [from_row(v) for v in run_row(codes[name].words, S)]
+        Sw = {G.CONST_BASE + k: v for k, v in enumerate(cv)}
+        Sw.update({G.IN_BASE + k: v for k, v in enumerate(vals)})
+        want = G.run_encoded(G.build_programs()[name].encode(), Sw)
+        assert got == want, name
+
+
+ORDER = ["MUL12", "SQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP"]
+
+
+def const_limbs(v):
+    return limbs(v)[:14]
+
+
+def render(check=True):
+    progs = G.build_programs()
+    codes = {k: encode(v) for k, v in progs.items()}
+    if check:
+        _checks(codes)
+    lines = ["// Generated by tools/gen_row_programs.py -- do not edit.",
+             "// Row-engine programs and constants (see the generator's docstring for the encoding).",
+             "#pragma once", "#include <stdint.h>", "",
+             f"#define LBR_IN {G.IN_BASE}", f"#define LBR_CONST {G.CONST_BASE}", f"#define LBR_TEMP {G.TEMP_BASE}",
+             f"#define LBR_C_B3 {G.C_B3}", f"#define LBR_C_INV2 {G.C_INV2}", f"#define LBR_C_FROB1 {G.C_FROB1}",
+             f"#define LBR_C_FROB2 {G.C_FROB2}", f"#define LBR_C_ZERO {G.C_ZERO}", f"#define LBR_N_CONST {N_CONST}",
+             f"#define LBR_INV_P336 {INV_P336.hex()}  // 2^336 / p, nearest double"]
+    image, maxtemp = [], 0
+    for name in ORDER:
+        c = codes[name]
+        maxtemp = max(maxtemp, c.ntemp)
+        lines.append(f"// {name}: {c.n_prods} products, {c.n_lins} linear tasks, {c.n_phases} phases, "
+                     f"{c.ntemp} temps, offset {len(image)}")
+        lines.append(f"#define LBR_{name} {len(image)}")
+        image += c.words
+        image += [0] * (-len(image) % 4)
+        if name == "FROB2":
+            lines.append(f"#define LBR_PROGS_FE {len(image)}")
+    lines.append(f"#define LBR_PROGS_ALL {len(image)}")
+    lines.append(f"#define LBR_MAX_TEMPS {maxtemp}")
+    lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_PROGS[{len(image)}] = "
+                 f"{{{', '.join(str(v) for v in image)}}};")
+    # constants: the CONST slots in row form, p, -p^-1 mod 2^392, and the conversion factors
+    cv = consts_values()
+    rows = [const_limbs(v * RP % P) for v in cv]
+    lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_CONST_LIMBS[{N_CONST}][16] = {{"
+                 + ", ".join("{" + ", ".join(str(x) for x in r + [0, 0]) + "}" for r in rows) + "};")
+
+    def arr(name, v, comment):
+        lines.append(f"// {comment}")
+        lines.append(f"#define {name} " + ", ".join(str(x) for x in const_limbs(v)))
+    arr("LBR_P_LIMBS", P, "p")
+    arr("LBR_PINV_LIMBS", PINV, "-p^-1 mod 2^392")
+    arr("LBR_K_IMPORT", pow(2, 400, P), "2^400 mod p: rp_mul(x_R, K) = the row form of a 2^384-Montgomery value")
+    arr("LBR_K_EXPORT", pow(2, 384, P), "2^384 mod p: rp_mul(x_row, K) = the 2^384-Montgomery value")
+    arr("LBR_K_PLAIN", pow(2, 784, P), "2^784 mod p: rp_mul(x, K) = the row form of a plain integer")
+    arr("LBR_ONE", RP % P, "1 in row form")
+    return progs, codes, "\n".join(lines) + "\n"
+
+
+def main():
+    progs, codes, text = render()
+    with open(OUT_PATH, "w") as fh:
+        fh.write(text)
+    for name in ORDER:
+        c = codes[name]
+        print(f"{name}: {c.n_prods} products, {c.n_phases} phases, {len(c.words)} words")
+    print("wrote", OUT_PATH)
+
+
+if __name__ == "__main__":
+    main()
