@@ -111,6 +111,12 @@ struct lb_engine {
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
   hipStream_t stream3 = nullptr;  // s3: pubkey aggregation + blinding, beside the signature decode
+  // batches of at most prio_max sets (a gossip block's proposer check, verifyOnMainThread, a
+  // light-client update) run on a second stream trio created at the device's greatest priority,
+  // so their kernels are not queued behind the bulk batches of the other engines
+  // (main_thread_1set_ms_under_load); created on first use.  LB_PRIO_MAX (0: off)
+  hipStream_t hp[3] = {nullptr, nullptr, nullptr};
+  uint32_t prio_max = 32;
   hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr, ev_pk = nullptr;
   std::mutex mu;
   // workspace
@@ -118,7 +124,8 @@ struct lb_engine {
       nodes, verdict, parts, ok, chunk_acc, chunk_status, fS;
   // message grouping (k_msg_*, k_gsum_*)
   dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
-      set_live, gacc, gp_aff, gp_inf;
+      set_live, gacc, gp_aff, gp_inf, chunk_root;
+  uint32_t gmax_chunks = 0;  // chunks of the largest root (the k_gsum_tree levels), read back with n_u
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
   // parked lone-lane state: k_hash_finish's points (4 x 72 words per launched lane), k_miller_lane's T
@@ -147,6 +154,9 @@ struct lb_engine {
   // flight on the device, else 8 lanes per root (k_miller_g8).  LB_MILLER_WAVE_MAX;
   // LB_MILLER_FORM = lane | g8 pins the large-batch form (default: by device load).
   uint32_t miller_wave_max = 2048;
+  // ... and up to this many roots (tree nodes of a level) on the row engine (lb_row.h: one 16-wave
+  // workgroup per item, the products split over 16-lane rows; latency).  LB_ROW_MAX.
+  uint32_t row_max = 8;
   int miller_form = 0;  // 0 by load, 1 lane, 2 g8
   // one-lane Miller loops with f and a temporary in LDS (two waves per CU) up to this many roots,
   // f alone in LDS (one wave per SIMD) above: LB_MILLER_LDS3_MAX (lb_kernels.h k_miller_lane)
@@ -363,6 +373,8 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   int prio_least = 0, prio_greatest = 0;
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
+  if (const char* rm = getenv("LB_ROW_MAX")) e->row_max = (uint32_t)strtoul(rm, nullptr, 10);
+  if (const char* pm = getenv("LB_PRIO_MAX")) e->prio_max = (uint32_t)strtoul(pm, nullptr, 10);
   if (const char* ml = getenv("LB_MILLER_LDS3_MAX")) e->miller_lds3_max = (uint32_t)strtoul(ml, nullptr, 10);
   if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
@@ -385,7 +397,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void**)&e->h_nu, 4, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_nu, 8, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_flag, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
@@ -442,7 +454,7 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->ok, &e->chunk_acc, &e->chunk_status, &e->fS, &e->table, &e->msg_tab,
                   &e->rep_of, &e->uid_of, &e->uniq_set, &e->n_u, &e->set_uid, &e->gcnt, &e->gpos, &e->goff,
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
-                  &e->gp_inf, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
+                  &e->gp_inf, &e->chunk_root, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
                   &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->wsum, &e->park, &e->set_spec, &e->live_flag, &e->pk_aff, &e->y_root, &e->kzg_g1,
                   &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set};
   for (dbuf* b : bufs) b->release();
@@ -464,6 +476,11 @@ void lb_engine_destroy(lb_engine* e) {
   hipStreamDestroy(e->stream2);
   hipStreamDestroy(e->stream3);
   hipStreamDestroy(e->stream);
+  for (hipStream_t h : e->hp)
+    if (h) {
+      hipStreamSynchronize(h);
+      hipStreamDestroy(h);
+    }
   {
     std::lock_guard<std::mutex> lk(g_engine_mu);
     g_engine_count[e->device]--;
@@ -726,9 +743,14 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
   {
     stage_scope sc(e, ST_GSUM, s1);
     // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
-    hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nuh + n / LB_GROUP_CHUNK)), dim3(LB_TPB), 0, s1, n, nu,
+    const uint32_t nch = nuh + n / LB_GROUP_CHUNK;
+    hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu,
                        e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
                        e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
+    // the per-root tree over the chunk sums (levels until one partial per root is left)
+    for (uint32_t st = 1; st < e->gmax_chunks; st *= LB_GSUM_FAN)
+      hipLaunchKernelGGL(k_gsum_tree, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                         e->chunk_root.as<uint32_t>(), st, e->gacc.as<uint32_t>());
     hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                        e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
   }
@@ -736,7 +758,10 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
     stage_scope sc(e, ST_MILLER, s1);
     const bool shared = e->miller_form == 1 ||
                         (e->miller_form == 0 && !device_alone(e));
-    if (nuh <= e->miller_wave_max) {
+    if (nuh <= e->row_max) {
+      hipLaunchKernelGGL(k_miller_row, dim3(nuh), dim3(LBR_NT), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
+                         e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
+    } else if (nuh <= e->miller_wave_max) {
       hipLaunchKernelGGL(k_miller_wave, dim3(nuh), dim3(64), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                          e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
     } else if (shared) {
@@ -758,8 +783,12 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
   }
   {
     stage_scope sc(e, ST_TREE_P, s1);
-    for (uint32_t lo = mu / 2; lo >= 1; lo /= 2)
-      hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
+    for (uint32_t lo = mu / 2; lo >= 1; lo /= 2) {
+      if (lo <= e->row_max)
+        hipLaunchKernelGGL(k_tree_up_row, dim3(lo), dim3(LBR_NT), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
+    }
   }
   return hipGetLastError();
 }
@@ -795,11 +824,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   LB_HIP(e->fS.ensure(sizeof(fp12)));
   LB_HIP(e->msg_tab.ensure((size_t)cap * 4));
   dbuf* per_set[] = {&e->rep_of, &e->uid_of, &e->uniq_set, &e->set_uid, &e->gcnt, &e->gpos, &e->chunk_beg,
-                     &e->chunk_end, &e->members, &e->set_live, &e->gp_inf};
+                     &e->chunk_end, &e->members, &e->set_live, &e->gp_inf, &e->chunk_root};
   for (dbuf* d : per_set) LB_HIP(d->ensure((size_t)ns * 4));
   LB_HIP(e->goff.ensure((size_t)(ns + 1) * 4));
   LB_HIP(e->gch.ensure((size_t)(ns + 1) * 4));
-  LB_HIP(e->n_u.ensure(4));
+  LB_HIP(e->n_u.ensure(8));
   LB_HIP(e->gacc.ensure((size_t)ns * sizeof(g1j)));
   LB_HIP(e->gp_aff.ensure((size_t)ns * sizeof(g1a)));
   const uint32_t bcap = (2 * LB_MSM_W * ns) / LB_MSM_CHUNK + LB_MSM_NB;  // bucket chunks, upper bound
@@ -895,15 +924,17 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
                          e->gpos.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, (uint32_t)LB_GROUP_CHUNK, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
-                         e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>());
+                         e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
+                         e->chunk_root.as<uint32_t>(), e->n_u.as<uint32_t>() + 1);
       hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
       // distinct-root count to the host: the per-root kernels below are launched over it (a
       // launch over the set count would size their private-segment scratch for n lanes)
-      LB_HIP(hipMemcpyAsync(e->h_nu, e->n_u.p, 4, hipMemcpyDeviceToHost, s1));
+      LB_HIP(hipMemcpyAsync(e->h_nu, e->n_u.p, 8, hipMemcpyDeviceToHost, s1));
       LB_HIP(hipStreamSynchronize(s1));
     }
-    const uint32_t nuh = *e->h_nu;
+    const uint32_t nuh = e->h_nu[0];
+    e->gmax_chunks = e->h_nu[1];
     if (nuh == 0 || nuh > n) return LB_ERR_DEVICE;
     mu = 1;
     while (mu < nuh) mu <<= 1;
@@ -962,7 +993,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s2, nullptr, (uint32_t)LB_MSM_NB, (uint32_t)LB_MSM_CHUNK,
                          e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
-                         e->bchunk_end.as<uint32_t>());
+                         e->bchunk_end.as<uint32_t>(), nullptr, nullptr);
       hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->scalars.as<uint64_t>(),
                          e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), e->boff.as<uint32_t>(),
                          e->bcursor.as<uint32_t>(), e->bmembers.as<uint32_t>());
@@ -999,7 +1030,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   // ---- s2: ML(-G1, S_root)
   {
     stage_scope sc(e, ST_ML_S, s2);
-    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
+    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(LB_FE_TPB), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
   }
   LB_HIP(hipEventRecord(e->ev_s, s2));
   LB_HIP(hipStreamWaitEvent(s1, e->ev_s, 0));  // join
@@ -1287,7 +1318,7 @@ static int32_t search_round(lb_engine* e, const search_ctx& x, const std::vector
       }
       hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nullptr, nb, schunk, e->bcnt.as<uint32_t>(),
                          e->boff.as<uint32_t>(), e->bch.as<uint32_t>(), e->bchunk_beg.as<uint32_t>(),
-                         e->bchunk_end.as<uint32_t>());
+                         e->bchunk_end.as<uint32_t>(), nullptr, nullptr);
       if (T) {
         if (w4)
           hipLaunchKernelGGL(k_smsm_scatter<LB_MSM_W>, dim3(nblk(T)), dim3(LB_TPB), 0, s1, T, cm, ma,
@@ -1590,9 +1621,41 @@ static void finish_profile(lb_engine* e) {
   }
 }
 
+// The engine's streams for the duration of one call: the high-priority trio for small batches
+// (created once, at the greatest priority), the normal trio otherwise.  The caller holds e->mu.
+struct stream_choice {
+  lb_engine* e;
+  bool swapped = false;
+  stream_choice(lb_engine* e_, uint32_t n_sets) : e(e_) {
+    if (!e->prio_max || n_sets > e->prio_max) return;
+    if (!e->hp[0]) {
+      int least = 0, greatest = 0;
+      hipDeviceGetStreamPriorityRange(&least, &greatest);
+      for (int k = 0; k < 3; k++)
+        if (hipStreamCreateWithPriority(&e->hp[k], hipStreamNonBlocking, greatest) != hipSuccess) {
+          for (int j = 0; j <= k; j++)
+            if (e->hp[j]) hipStreamDestroy(e->hp[j]);
+          e->hp[0] = e->hp[1] = e->hp[2] = nullptr;
+          return;  // the normal streams still work
+        }
+    }
+    std::swap(e->stream, e->hp[0]);
+    std::swap(e->stream2, e->hp[1]);
+    std::swap(e->stream3, e->hp[2]);
+    swapped = true;
+  }
+  ~stream_choice() {
+    if (!swapped) return;
+    std::swap(e->stream, e->hp[0]);
+    std::swap(e->stream2, e->hp[1]);
+    std::swap(e->stream3, e->hp[2]);
+  }
+};
+
 // caller holds e->mu
 static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars, int32_t* out_job) {
   LB_HIP(hipSetDevice(e->device));
+  stream_choice sch(e, b->n_sets);
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
   uint32_t m = 1, mu = 1;
@@ -1604,7 +1667,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   {
     stage_scope sc(e, ST_ROOT, e->stream);
     LB_HIP(e->y_root.ensure(576));
-    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
   }
   LB_HIP(hipGetLastError());
@@ -1649,7 +1712,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   LB_HIP(e->parts.ensure(576));
   {
     stage_scope sc(e, ST_ROOT, e->stream);
-    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->parts.as<uint8_t>());
   }
   LB_HIP(hipGetLastError());
@@ -1676,7 +1739,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   LB_HIP(e->verdict.ensure(4));
   LB_HIP(e->y_root.ensure(576));
   // this shard's own root check: a passing shard is done, a failing one searches from it
-  hipLaunchKernelGGL(k_root_check, dim3(1), dim3(64), 0, e->stream, mu, e->treeP.as<uint32_t>(), e->fS.as<uint32_t>(),
+  hipLaunchKernelGGL(k_root_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(), e->fS.as<uint32_t>(),
                      e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
   LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(nj);
@@ -1702,7 +1765,7 @@ extern "C" int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials5
   LB_HIP(e->parts.ensure((size_t)(n ? n : 1) * 576));
   LB_HIP(e->ok.ensure(4));
   if (n) LB_HIP(hipMemcpyAsync(e->parts.p, partials576, (size_t)n * 576, hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(64), 0, e->stream, n, e->parts.as<uint8_t>(),
+  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, n, e->parts.as<uint8_t>(),
                      e->ok.as<int32_t>());
   LB_HIP(hipGetLastError());
   LB_HIP(hipMemcpyAsync(ok, e->ok.p, 4, hipMemcpyDeviceToHost, e->stream));

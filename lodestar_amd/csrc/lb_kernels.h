@@ -127,6 +127,18 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 
 #include "lb_wave.h"
+#include "lb_row.h"
+// LB_ROW_FE=1: the final exponentiations, ML(-G1, S), the small-batch per-root Miller loops and the
+// product tree run on the row engine (lb_row.h, one Fp product per 16-lane row, 4-wave
+// workgroups); 0: the wave engine (lb_wave.h, one product per lane, one wave)
+#ifndef LB_ROW_FE
+#define LB_ROW_FE 1
+#endif
+#if LB_ROW_FE
+#define LB_FE_TPB LBR_NT
+#else
+#define LB_FE_TPB 64
+#endif
 #include "lb_group_exec.h"
 #include "lb_group.h"
 #include "lb_ssz.h"
@@ -1015,7 +1027,10 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // slot 0xffffffff), probed from a keyed hash of the root (key from the engine's CSPRNG, so crafted
 // roots cannot be aimed at one probe chain); equality is decided on all 32 bytes.  A slot, once
 // claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
-#define LB_GROUP_CHUNK 32  // members summed per lane in k_gsum_chunks
+#ifndef LB_GROUP_CHUNK
+#define LB_GROUP_CHUNK 4  // members summed per lane in k_gsum_chunks (then the k_gsum_tree levels)
+#endif
+#define LB_GSUM_FAN 4     // partial sums combined per lane and level in k_gsum_tree
 #ifndef LB_MSM_CHUNK
 #ifndef LB_MSM_CHUNK
 #define LB_MSM_CHUNK 16  // bucket members summed per lane in k_msm_chunks (the batch MSM's serial chain)
@@ -1110,18 +1125,23 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_count(uint32_t n, const uint32_t
 __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ n_u, uint32_t nu_const, uint32_t chunk,
                                                    const uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ goff, uint32_t* __restrict__ gch,
-                                                   uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end) {
-  __shared__ uint32_t s_m[1024], s_c[1024];
+                                                   uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end,
+                                                   uint32_t* __restrict__ chunk_root, uint32_t* __restrict__ max_chunks) {
+  __shared__ uint32_t s_m[1024], s_c[1024], s_x;
   const uint32_t nu = n_u ? *n_u : nu_const, t = threadIdx.x, per = (nu + 1023u) / 1024u;
   const uint32_t a = min(t * per, nu), b = min(a + per, nu);
-  uint32_t sm = 0, sc = 0;
+  uint32_t sm = 0, sc = 0, mx = 0;
   for (uint32_t u = a; u < b; u++) {
     sm += cnt[u];
-    sc += (cnt[u] + chunk - 1) / chunk;
+    const uint32_t cu = (cnt[u] + chunk - 1) / chunk;
+    sc += cu;
+    mx = max(mx, cu);
   }
+  if (t == 0) s_x = 0;
   s_m[t] = sm;
   s_c[t] = sc;
   __syncthreads();
+  if (max_chunks) atomicMax(&s_x, mx);
   for (uint32_t d = 1; d < 1024; d <<= 1) {
     const uint32_t vm = t >= d ? s_m[t - d] : 0u, vc = t >= d ? s_c[t - d] : 0u;
     __syncthreads();
@@ -1137,6 +1157,7 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     for (uint32_t k = 0; k < c; k += chunk) {
       chunk_beg[oc] = om + k;
       chunk_end[oc] = om + min(k + chunk, c);
+      if (chunk_root) chunk_root[oc] = u;
       oc++;
     }
     om += c;
@@ -1145,6 +1166,7 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     goff[nu] = s_m[1023];
     gch[nu] = s_c[1023];
   }
+  if (max_chunks && t == 0) *max_chunks = s_x;  // (the atomics completed before the scan's barriers)
 }
 #endif  // LB_KG
 
@@ -2149,7 +2171,29 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
 }
 #endif  // LB_KG
 
-// P_u = sum of the group's chunk sums, to affine (one batched inversion per block); gp_inf[u]
+// One level of the per-root sum tree over the chunk sums (in place, strided): at stride s, the
+// lane of chunk c with (c - gch[u]) a multiple of LB_GSUM_FAN s adds the partials at c + k s,
+// k = 1 .. LB_GSUM_FAN - 1, of its own root; after the levels with s < max chunks per root,
+// gacc[gch[u]] holds P_u.  The reads of one lane, [c, c + FAN s), are nobody else's writes.
+// (The serial chains this replaces, up to 32 members per lane and then up to 32 chunk sums per
+// root on one lane, were the longest per-root latency of a batch alone: VERDICT r4.)
+#if LB_KG(4)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_tree(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                      const uint32_t* __restrict__ gch,
+                                                      const uint32_t* __restrict__ chunk_root, uint32_t s,
+                                                      uint32_t* __restrict__ gacc) {
+  const uint32_t c = lb_tid();
+  if (c >= gch[*n_u]) return;
+  const uint32_t u = chunk_root[c], base = gch[u], end = gch[u + 1];
+  if ((c - base) % (LB_GSUM_FAN * s) != 0 || c + s >= end) return;
+  jac<lb_g1f> acc = jac_as<lb_g1f>(soa_ld<g1j>(gacc, n, c));
+  LB_UNROLL for (uint32_t k = 1; k < LB_GSUM_FAN; k++)
+    if (c + k * s < end) acc = jac_add_i<lb_g1f, true>(acc, jac_as<lb_g1f>(soa_ld<g1j>(gacc, n, c + k * s)));
+  soa_st(gacc, n, c, jac_as<fp>(acc));
+}
+#endif  // LB_KG
+
+// P_u (the tree's root at gacc[gch[u]]) to affine (one batched inversion per block); gp_inf[u]
 // flags P_u = infinity (no live member, or members cancelling), whose Miller value is 1.
 #if LB_KG(4)
 __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, const uint32_t* __restrict__ n_u,
@@ -2162,8 +2206,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
   if (blockIdx.x * LB_INV_TPB >= nu) return;  // whole block idle (uniform)
   const bool act = u < nu;
   g1j acc = jac_infinity<fp>();
-  if (act)
-    for (uint32_t c = gch[u]; c < gch[u + 1]; c++) acc = jac_add(acc, soa_ld<g1j>(gacc, n, c));
+  if (act) acc = soa_ld<g1j>(gacc, n, gch[u]);
   const bool zero = jac_is_inf(acc);
   const fp zi = fp_inv_block(act && !zero ? acc.z : fp_one());
   if (!act) return;
@@ -2213,9 +2256,84 @@ __global__ void __launch_bounds__(64) k_tree_up_U(uint32_t m, uint32_t lo, const
 }
 #endif  // LB_KG
 
+// Row-engine forms of the per-root Miller loop and a product-tree level for batches with few
+// distinct roots (latency: one 16-wave workgroup per root / node, lb_row.h); the engine picks
+// them up to lb_engine::row_max items and the wave / lane forms above (less work per item) beyond.
+#if LB_KG(10)
+__global__ void __launch_bounds__(LBR_NT) k_miller_row(uint32_t n, uint32_t m, const uint32_t* __restrict__ n_u,
+                                                        const uint32_t* __restrict__ gp_aff,
+                                                        const uint32_t* __restrict__ gp_inf,
+                                                        const uint32_t* __restrict__ h_aff, uint32_t* __restrict__ treeP) {
+  LBR_SHARED_MILLER(S);
+  const uint32_t u = blockIdx.x;
+  if (u >= *n_u) return;
+  const int t = threadIdx.x;
+  r_init(S, LBR_MILLER_COUNT, LBR_MILLER_FIRST);
+  if (gp_inf[u] != 0) {  // uniform
+    r_set_one(S, LBR_A(0));
+  } else {
+    if (t < 6) {
+      const uint32_t* base = t < 2 ? gp_aff + (size_t)12 * t * n : h_aff + (size_t)12 * (t - 2) * n;
+      fp v;
+      LB_UNROLL for (int w = 0; w < 12; w++) v.v[w] = base[(size_t)w * n + u];
+      r_stage_fp(S, t, v);
+    }
+    r_sync();
+    r_import_staged(S, LBR_PT, 6);
+    r_miller(S, LBR_A(0));
+  }
+  r_store_soa12(S, LBR_A(0), treeP, 2 * m, m + u);
+}
+#endif  // LB_KG
+#if LB_KG(10)
+__global__ void __launch_bounds__(LBR_NT) k_tree_up_row(uint32_t m, uint32_t lo, const uint32_t* __restrict__ n_u,
+                                                      uint32_t* __restrict__ treeP) {
+  LBR_SHARED(S);
+  const uint32_t i = lo + blockIdx.x, span = m / lo, start = blockIdx.x * span, nu = *n_u;
+  if (start >= nu) return;
+  r_init(S);
+  r_load_soa12(S, LBR_A(0), treeP, 2 * m, 2 * i);
+  if (start + span / 2 < nu) {
+    r_load_soa12(S, LBR_A(1), treeP, 2 * m, 2 * i + 1);
+    r_mul(S, LBR_A(0), LBR_A(0), LBR_A(1));
+  }
+  r_store_soa12(S, LBR_A(0), treeP, 2 * m, i);
+}
+#endif  // LB_KG
+
 // fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
 // computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
 #if LB_KG(5)
+#if LB_ROW_FE
+__global__ void __launch_bounds__(LBR_NT) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
+  LBR_SHARED_MILLER(S);
+  __shared__ int s_inf;
+  __shared__ fp pv[6];
+  r_init(S, LBR_MILLER_COUNT, LBR_MILLER_FIRST);
+  if (threadIdx.x == 0) {
+    const g2j Sj = soa_ld<g2j>(treeS, 2 * m, 1);
+    s_inf = jac_is_inf(Sj) ? 1 : 0;
+    if (!s_inf) {
+      g2a a;
+      g2_to_aff_inl(a, Sj);
+      pv[0] = fp_load(LB_G1X);
+      pv[1] = fp_load(LB_G1NEGY);
+      pv[2] = a.x.c0;
+      pv[3] = a.x.c1;
+      pv[4] = a.y.c0;
+      pv[5] = a.y.c1;
+    }
+  }
+  r_sync();
+  if (s_inf) {
+    r_set_one(S, LBR_A(7));
+  } else {
+    r_import_fps(S, LBR_PT, pv, 6);
+    r_miller(S, LBR_A(7));
+  }
+  r_store_soa12(S, LBR_A(7), fS, 1, 0);
+}
+#else
 __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
   LBW_SHARED_ML(S);
   __shared__ int s_inf;
@@ -2242,11 +2360,27 @@ __global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restr
     w_miller(S, LBW_A(7));
   w_store_soa12(S, LBW_A(7), fS, 1, 0);
 }
+#endif
 #endif  // LB_KG
 
 // root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
 // (the FE value y goes to y_out for the invalid-set search)
 #if LB_KG(5)
+#if LB_ROW_FE
+__global__ void __launch_bounds__(LBR_NT) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                       const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
+                                                       uint32_t* __restrict__ y_out) {
+  LBR_SHARED(S);
+  r_init(S);
+  r_load_soa12(S, LBR_A(0), treeP, 2 * m, 1);
+  r_load_soa12(S, LBR_A(7), fS, 1, 0);
+  r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
+  r_final_exp(S, LBR_A(0), LBR_A(0));
+  const bool one = r_is_one(S, LBR_A(0));
+  r_store_soa12(S, LBR_A(0), y_out, 1, 0);
+  if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
+}
+#else
 __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
                                                    const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
                                                    uint32_t* __restrict__ y_out) {
@@ -2260,10 +2394,23 @@ __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* _
   w_store_soa12(S, LBW_A(0), y_out, 1, 0);
   if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
+#endif
 #endif  // LB_KG
 
 // root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
 #if LB_KG(5)
+#if LB_ROW_FE
+__global__ void __launch_bounds__(LBR_NT) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                         const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
+  LBR_SHARED(S);
+  r_init(S);
+  r_load_soa12(S, LBR_A(0), treeP, 2 * m, 1);
+  r_load_soa12(S, LBR_A(7), fS, 1, 0);
+  r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
+  r_export(S, LBR_A(0), 12);
+  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(r_fp_of_staged(S, threadIdx.x)));
+}
+#else
 __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
                                                      const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
   LBW_SHARED(S);
@@ -2273,9 +2420,34 @@ __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t*
   w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(w_ld(S, LBW_A(0) + threadIdx.x)));
 }
+#endif
 #endif  // LB_KG
 
 #if LB_KG(5)
+#if LB_ROW_FE
+__global__ void __launch_bounds__(LBR_NT) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
+                                                           int32_t* __restrict__ ok) {
+  LBR_SHARED(S);
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  r_init(S);
+  r_set_one(S, LBR_A(0));
+  for (uint32_t i = 0; i < n; i++) {
+    if (t < 12) {
+      fp x;
+      if (!fp_plain_from_be48(x, parts + (size_t)576 * i + 48 * t, 0xff)) atomicOr(&bad, 1);
+      r_stage_fp(S, t, fp_to_mont(x));
+    }
+    r_sync();
+    r_import_staged(S, LBR_A(7), 12);
+    r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
+  }
+  r_final_exp(S, LBR_A(0), LBR_A(0));
+  const bool one = r_is_one(S, LBR_A(0));
+  if (t == 0) *ok = (one && !bad) ? 1 : 0;
+}
+#else
 __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
                                                        int32_t* __restrict__ ok) {
   LBW_SHARED(S);
@@ -2297,6 +2469,7 @@ __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t
   bool one = w_is_one(S, LBW_A(0));
   if (lane == 0) *ok = (one && !bad) ? 1 : 0;
 }
+#endif
 #endif  // LB_KG
 
 // ---------------------------------------------------------------- pubkey aggregation only

@@ -1,0 +1,605 @@
+// Row engine: the Fp12 programs of lb_wave.h (final exponentiation, Miller loops, product-tree
+// nodes) with every Fp product split over one 16-lane ROW of a wave instead of one lane.
+//
+// Why: a lone lane runs one 381-bit Montgomery product in ~2 500 cycles (~630 dependent VALU
+// instructions), so a final exponentiation or a Miller loop on the wave engine is a chain of
+// ~1 us product phases plus the per-lane operand sums (12 LDS words per term).  Here lane k of a
+// row holds limb k of an element (14 signed 28-bit limbs; lanes 14, 15 hold 0): an operand sum is
+// one LDS word per term per lane, and a product is a systolic pass over the row (~200 VALU
+// instructions, the shifts by DPP row_shr / row_shl), so a phase of <= 16 products takes ~1/3 of
+// a lone-lane product on a 4-wave workgroup (16 rows, one wave per SIMD).
+//
+// Representation (tools/gen_row_programs.py mirrors it exactly): a slot holds an integer v in
+// (-2p, 2p) congruent to x R' (mod p), R' = 2^392, as v = sum_k l_k 2^(28 k) with l_0..l_12 in
+// [-1, 2^28 + 2) and l_13 a small signed top limb.  Slot s, limb k at LDS word 16 s + k.
+//
+// Product (rp_mul): x replicated in every lane of the row (14 registers), y distributed.
+//   columns of x y: lane k accumulates column k (lo) and column k + 16 (hi), 64-bit, while y
+//   shifts by row_shr:i / row_shl:(16 - i);
+//   m = (x y mod 2^392)(-p^-1) mod 2^392 from the low columns normalised to ~28-bit limbs;
+//   U = x y + m p; its low half is C 2^392 with C = ceil((U13 + U12 / 2^28 + U11 / 2^56) / 2^28)
+//   (the lower columns move that by < 2^-17); the result is U's high columns + C, normalised.
+//   |result| < |x y| / 2^392 + 1.0001 p.
+// Operand / linear sums: signed limb sums (64-bit), then q = floor(v / p) estimated from the top
+// two limbs in double precision (lane 13), broadcast over the row (ds_swizzle), v - q p: [0, p)
+// up to an error far below p.
+// Everything is collective over the workgroup (LBR_NT threads); one wave per SIMD.
+#pragma once
+#include "lb_pairing.h"
+#include "lb_row_progs.h"
+
+#ifndef LBR_WAVES
+#define LBR_WAVES 16  // one workgroup of 16 waves (4 per SIMD): a phase of <= 64 products in one round
+#endif
+#define LBR_NT (64 * LBR_WAVES)
+#define LBR_NROWS (4 * LBR_WAVES)
+#define LBR_PERSIST (LBR_TEMP + LBR_MAX_TEMPS)
+#define LBR_A(k) (LBR_PERSIST + 12 * (k))  // caller-owned Fp12 areas
+#define LBR_N_AREAS 8
+#define LBR_PT (LBR_PERSIST + 12 * LBR_N_AREAS)  // Miller loop: P (2), Q (4), T (6)
+#define LBR_XS (LBR_PT + 16)                     // staging slots for import / export (16)
+#define LBR_ROWX (LBR_XS + 16)                   // one operand slot per row
+#define LBR_SLOTS (LBR_ROWX + LBR_NROWS)
+#define LBR_SLOT_WORDS (16 * LBR_SLOTS)
+#define LBR_MISC 8  // words after the slots: [0] first staged program word, [1] flag, [2] scratch
+// The per-workgroup LDS block: the slots, misc words, the staged program image (a prefix / range
+// of LBR_PROGS).  LBR_SHARED_N(name, words)
+#define LBR_SHARED_N(name, nprog)                                                                 \
+  __shared__ __attribute__((aligned(16))) int32_t name##_lds[LBR_SLOT_WORDS + LBR_MISC + (nprog)]; \
+  int32_t* name = name##_lds
+#define LBR_SHARED(name) LBR_SHARED_N(name, LBR_PROGS_FE)
+#define LBR_SHARED_ML(name) LBR_SHARED_N(name, LBR_PROGS_ALL)
+#define LBR_MILLER_FIRST LBR_DBL_STEP
+#define LBR_MILLER_COUNT (LBR_PROGS_ALL - LBR_DBL_STEP)
+#define LBR_SHARED_MILLER(name) LBR_SHARED_N(name, LBR_MILLER_COUNT)
+static_assert(LBR_DBL_STEP >= LBR_PROGS_FE && LBR_ADD_STEP > LBR_DBL_STEP, "lb_row.h: program image order");
+
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
+
+__device__ __forceinline__ void r_sync() { __syncthreads(); }
+__device__ __forceinline__ int r_tid() { return threadIdx.x; }
+__device__ __forceinline__ int r_limb() { return threadIdx.x & 15; }
+__device__ __forceinline__ int r_row() { return threadIdx.x >> 4; }
+__device__ __forceinline__ lds_i32* r_lds(int32_t* S) { return (lds_i32*)S; }
+
+// ---------------------------------------------------------------- DPP within a row
+template <int CTRL>
+__device__ __forceinline__ int r_dpp(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);  // bound_ctrl: out-of-row sources read 0
+}
+template <int CTRL>
+__device__ __forceinline__ int64_t r_dpp64(int64_t v) {
+  const int lo = r_dpp<CTRL>((int)(uint32_t)(uint64_t)v), hi = r_dpp<CTRL>((int)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+#define LBR_SHR(n) (0x110 + (n))  // lane k <- lane k - n of the row (0 below the row)
+#define LBR_SHL(n) (0x100 + (n))  // lane k <- lane k + n of the row (0 above the row)
+// broadcast lane 13 of each row (ds_swizzle bit mode: lane' = (lane & 0x10) | 13 within 32)
+__device__ __forceinline__ int r_bcast13(int v) { return __builtin_amdgcn_ds_swizzle(v, 0x10 | (13 << 5)); }
+
+#define LBR_M28 0x0fffffff
+struct lbr_k {
+  static constexpr int P[14] = {LBR_P_LIMBS};
+  static constexpr int PINV[14] = {LBR_PINV_LIMBS};
+  static constexpr int K_EXPORT[14] = {LBR_K_EXPORT};
+  static constexpr int K_PLAIN[14] = {LBR_K_PLAIN};
+  static constexpr int ONE[14] = {LBR_ONE};
+};
+// p's limb for this lane (0 in lanes 14, 15)
+__device__ __forceinline__ int r_plimb(int k) {
+  int v = 0;
+  LB_UNROLL for (int i = 0; i < 14; i++) v = k == i ? lbr_k::P[i] : v;
+  return v;
+}
+
+// Two carry rounds: 64-bit (the carry split in two 28-bit pieces), then 32-bit.  KEEP: limb 13
+// keeps its whole value and takes limb 12's carry whole (a value, not a residue mod 2^392);
+// otherwise carries out of limb 13 are dropped (mod 2^392).  Lanes 14, 15: 0 with KEEP.
+template <bool KEEP>
+__device__ __forceinline__ int r_norm(int64_t v, int k) {
+  const int64_t q = v >> 28;
+  int l = (int)(v & LBR_M28);
+  int qlo = (int)(q & LBR_M28), qhi = (int)(q >> 28);
+  if (KEEP) {
+    if (k == 12) {
+      qlo = (int)q;
+      qhi = 0;
+    }
+    if (k >= 13) {
+      l = k == 13 ? (int)v : 0;
+      qlo = qhi = 0;
+    }
+  }
+  l += r_dpp<LBR_SHR(1)>(qlo) + r_dpp<LBR_SHR(2)>(qhi);
+  int c = l >> 28, l2 = l & LBR_M28;
+  if (KEEP && k >= 13) {
+    c = 0;
+    l2 = k == 13 ? l : 0;
+  }
+  return l2 + r_dpp<LBR_SHR(1)>(c);
+}
+
+// lo += sum_i X[i] * y[k - i], hi += sum_{i>=1} X[i] * y[k + 16 - i]  (X replicated / constant);
+// even and odd terms into separate accumulators (two independent MAD chains)
+template <int I, bool HI, class XS>
+__device__ __forceinline__ void r_sys(const XS& x, int y, int64_t (&lo)[2], int64_t (&hi)[2]) {
+  if constexpr (I < 14) {
+    if constexpr (I == 0) {
+      lo[0] += (int64_t)x[0] * y;
+    } else {
+      lo[I & 1] += (int64_t)x[I] * r_dpp<LBR_SHR(I)>(y);
+      if constexpr (HI) hi[I & 1] += (int64_t)x[I] * r_dpp<LBR_SHL(16 - I)>(y);
+    }
+    r_sys<I + 1, HI>(x, y, lo, hi);
+  }
+}
+struct r_cx_p {
+  __device__ __forceinline__ int operator[](int i) const { return lbr_k::P[i]; }
+};
+struct r_cx_pinv {
+  __device__ __forceinline__ int operator[](int i) const { return lbr_k::PINV[i]; }
+};
+
+// The row Montgomery product of x (replicated: x[0..13] in every lane of the row) and y (lane k:
+// limb k, lanes 14, 15: 0): this lane's limb of x y / 2^392 (mod p).
+template <class XS>
+__device__ __forceinline__ int rp_mul(const XS& x, int y, int k) {
+  int64_t l2[2] = {0, 0}, h2[2] = {0, 0};
+  r_sys<0, true>(x, y, l2, h2);
+  int64_t lo = l2[0] + l2[1];
+  // m = (x y mod 2^392) (-p^-1) mod 2^392
+  int t = r_norm<false>(lo, k);
+  t = k < 14 ? t : 0;
+  int64_t m2[2] = {0, 0}, dummy[2] = {0, 0};
+  r_sys<0, false>(r_cx_pinv{}, t, m2, dummy);
+  int m = r_norm<false>(m2[0] + m2[1], k);
+  m = k < 14 ? m : 0;
+  // U = x y + m p
+  l2[0] = lo;
+  l2[1] = 0;
+  r_sys<0, true>(r_cx_p{}, m, l2, h2);
+  lo = l2[0] + l2[1];
+  const int64_t hi = h2[0] + h2[1];
+  // carry of the low half (a multiple of 2^392) into column 14
+  const int64_t u13 = r_dpp64<LBR_SHR(1)>(lo), u12 = r_dpp64<LBR_SHR(2)>(lo), u11 = r_dpp64<LBR_SHR(3)>(lo);
+  const int64_t E = u13 + (u12 >> 28) + (u11 >> 56);
+  const int64_t C = (E + LBR_M28) >> 28;
+  const int64_t w = k == 14 ? lo + C : (k == 15 ? lo : 0);
+  const int64_t r = r_dpp64<LBR_SHL(14)>(w) + r_dpp64<LBR_SHR(2)>(hi);
+  return r_norm<true>(r, k);
+}
+struct r_cx_arr {
+  const int* a;
+  __device__ __forceinline__ int operator[](int i) const { return a[i]; }
+};
+template <int N>
+struct r_cx_const {
+  const int (&a)[N];
+  __device__ __forceinline__ int operator[](int i) const { return a[i]; }
+};
+
+// limb-sum reduction: v (64-bit limb sums) -> v - q p with q = floor(v / p) from the top limbs
+__device__ __forceinline__ int r_reduce(int64_t acc, int k) {
+  const int64_t a12 = r_dpp64<LBR_SHR(1)>(acc);  // lane 13 sees limb 12
+  const double w = (double)acc * 268435456.0 + (double)a12;
+  int q = (int)floor(w * LBR_INV_P336);
+  q = r_bcast13(q);
+  acc -= (int64_t)q * r_plimb(k);
+  return r_norm<true>(acc, k);
+}
+
+// operand / linear sum over `n` (<= 8 * NB) (slot, coef) pairs at LDS words rec[0..n): the pair
+// words of a block of 8 and then their 8 limbs are loaded together (one LDS round trip each per
+// block instead of two per term)
+template <int NB>
+__device__ __forceinline__ int64_t r_acc(const lds_i32* S, const lds_i32* rec, int n, int k) {
+  int64_t acc = 0;
+  LB_UNROLL for (int b = 0; b < NB; b++) {
+    if (8 * b < n) {
+      int w[8], v[8];
+      LB_UNROLL for (int j = 0; j < 8; j++) w[j] = 8 * b + j < n ? rec[8 * b + j] : 0;
+      LB_UNROLL for (int j = 0; j < 8; j++) v[j] = 8 * b + j < n ? S[16 * (w[j] & 0xffff) + k] : 0;
+      LB_UNROLL for (int j = 0; j < 8; j++) acc += (int64_t)(w[j] >> 16) * v[j];
+    }
+  }
+  return acc;
+}
+template <int NB>
+__device__ __forceinline__ int r_sum(const lds_i32* S, const lds_i32* rec, int n, int k) {
+  return r_reduce(r_acc<NB>(S, rec, n, k), k);
+}
+// a product operand: with a coefficient sum <= 16 (phase flag clear) only the limb carries run
+__device__ __forceinline__ int r_operand(const lds_i32* S, const lds_i32* rec, int n, int k, bool red) {
+  const int64_t acc = r_acc<1>(S, rec, n, k);
+  return red ? r_reduce(acc, k) : r_norm<true>(acc, k);
+}
+
+__device__ __forceinline__ void r_load_rep(const lds_i32* S, int slot, int (&x)[14]) {
+  const lds_i32x4* q = (const lds_i32x4*)(S + 16 * slot);
+  const i32x4 a = q[0], b = q[1], c = q[2], d = q[3];
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w;
+  x[12] = d.x; x[13] = d.y;
+}
+
+// base of the staged program image as seen from LDS (words below `first` are never used)
+__device__ __forceinline__ const lds_i32* r_progs(int32_t* S) {
+  const lds_i32* s = r_lds(S);
+  return s + LBR_SLOT_WORDS + LBR_MISC - s[LBR_SLOT_WORDS + 0];
+}
+
+// Run one program (offset `off` in the image): inputs already in IN, outputs left in the temps
+// the header lists.
+__device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
+  lds_i32* S = r_lds(S_generic);
+  const lds_i32* prog = r_progs(S_generic) + off;
+  const int k = r_limb(), row = r_row();
+  const int nph = __builtin_amdgcn_readfirstlane(prog[0]), nout = __builtin_amdgcn_readfirstlane(prog[1]);
+  int pos = 2 + nout;
+  for (int ph = 0; ph < nph; ph++) {
+    const int h0 = __builtin_amdgcn_readfirstlane(prog[pos]), h1 = __builtin_amdgcn_readfirstlane(prog[pos + 1]);
+    pos += 2;
+    const int kind = h0 & 0xff, flags = (h0 >> 8) & 0xff, n = h0 >> 16;
+    const int nx = h1 & 0xffff, ny = h1 >> 16;
+    if (kind == 0) {
+      const int rs = 1 + nx + ny;
+      for (int base = 0; base < n; base += LBR_NROWS) {
+        const int t = base + row;
+        if (t < n) {
+          const lds_i32* rec = prog + pos + t * rs;
+          const int dst = rec[0];
+          const int y = (flags & 2) ? S[16 * (rec[1 + nx] & 0xffff) + k] : r_operand(S, rec + 1 + nx, ny, k, flags & 8);
+          int xs;
+          if (flags & 1) {
+            xs = rec[1] & 0xffff;
+          } else {
+            xs = LBR_ROWX + row;
+            S[16 * xs + k] = r_operand(S, rec + 1, nx, k, flags & 4);
+          }
+          int x[14];
+          r_load_rep(S, xs, x);
+          S[16 * dst + k] = rp_mul(x, y, k);
+        }
+      }
+      pos += n * rs;
+    } else {
+      const int rs = 1 + nx;
+      for (int base = 0; base < n; base += LBR_NROWS) {
+        const int t = base + row;
+        if (t < n) {
+          const lds_i32* rec = prog + pos + t * rs;
+          S[16 * rec[0] + k] = r_sum<3>(S, rec + 1, nx, k);
+        }
+      }
+      pos += n * rs;
+    }
+    r_sync();
+#ifdef LBR_PHASE_HOOK
+    LBR_PHASE_HOOK(ph, kind, n);
+#endif
+  }
+}
+
+// ---------------------------------------------------------------- element moves (limb-parallel)
+// dst[e] = src(e) for e < n (src(e) a slot index; every source read before any write)
+template <class F>
+__device__ __forceinline__ void r_gather(int32_t* S_generic, int dst, int n, F src) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row();
+  constexpr int J = (32 + LBR_NROWS - 1) / LBR_NROWS;  // n <= 32
+  int v[J];
+  LB_UNROLL for (int j = 0; j < J; j++) {
+    const int e = row + LBR_NROWS * j;
+    if (e < n) v[j] = S[16 * src(e) + k];
+  }
+  r_sync();
+  LB_UNROLL for (int j = 0; j < J; j++) {
+    const int e = row + LBR_NROWS * j;
+    if (e < n) S[16 * (dst + e) + k] = v[j];
+  }
+  r_sync();
+}
+__device__ __forceinline__ void r_copy(int32_t* S, int dst, int src, int n) {
+  r_gather(S, dst, n, [&](int e) { return src + e; });
+}
+__device__ __forceinline__ void r_out(int32_t* S, int off, int first, int n, int dst) {
+  const lds_i32* prog = r_progs(S) + off;
+  r_gather(S, dst, n, [&](int e) { return prog[2 + first + e]; });
+}
+__device__ __forceinline__ void r_set_one(int32_t* S_generic, int dst) {
+  lds_i32* S = r_lds(S_generic);
+  const int t = r_tid();
+  if (t < 12 * 16) {
+    const int e = t >> 4, k = t & 15;
+    int v = 0;
+    LB_UNROLL for (int i = 0; i < 14; i++) v = (e == 0 && k == i) ? lbr_k::ONE[i] : v;
+    S[16 * (dst + e) + k] = v;
+  }
+  r_sync();
+}
+// dst = conj(a): coefficients of w negated (limb-wise: the value stays in (-2p, 2p))
+__device__ __forceinline__ void r_conj(int32_t* S_generic, int dst, int a) {
+  lds_i32* S = r_lds(S_generic);
+  const int t = r_tid();
+  int v = 0;
+  if (t < 12 * 16) {
+    v = S[16 * (a + (t >> 4)) + (t & 15)];
+    if ((t >> 4) >= 6) v = -v;
+  }
+  r_sync();
+  if (t < 12 * 16) S[16 * (dst + (t >> 4)) + (t & 15)] = v;
+  r_sync();
+}
+
+// ---------------------------------------------------------------- import / export (one lane per element)
+// The raw limbs of a 2^384-Montgomery element's value times 2^8 (= x 2^392, < 2^389) into staging
+// slot LBR_XS + e; r_import_staged reduces them (quotient estimate) into dst + e.
+__device__ __forceinline__ void r_stage_fp(int32_t* S_generic, int e, const fp& a) {
+  lds_i32* S = r_lds(S_generic);
+  S[16 * (LBR_XS + e) + 0] = (int)((a.v[0] << 8) & LBR_M28);
+  LB_UNROLL for (int k = 1; k < 14; k++) S[16 * (LBR_XS + e) + k] = (int)lb_bits28(a.v, 28 * k - 8);
+  S[16 * (LBR_XS + e) + 14] = 0;
+  S[16 * (LBR_XS + e) + 15] = 0;
+}
+__device__ __forceinline__ void r_import_staged(int32_t* S_generic, int dst, int n) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb();
+  for (int e = r_row(); e < n; e += LBR_NROWS) S[16 * (dst + e) + k] = r_reduce((int64_t)S[16 * (LBR_XS + e) + k], k);
+  r_sync();
+}
+// canonical 2^384-Montgomery words of the signed limb value sum_k l_k 2^(28 k), |v| < 4p
+__device__ __forceinline__ fp r_canon(const int32_t* l) {
+  int32_t n[14];
+  int64_t c = 0;
+  LB_UNROLL for (int k = 0; k < 13; k++) {
+    const int64_t v = (int64_t)l[k] + c;
+    n[k] = (int32_t)(v & LBR_M28);
+    c = v >> 28;
+  }
+  n[13] = (int32_t)((int64_t)l[13] + c);
+  for (int it = 0; it < 4 && n[13] < 0; it++) {  // add p
+    int64_t cc = 0;
+    LB_UNROLL for (int k = 0; k < 14; k++) {
+      const int64_t v = (int64_t)n[k] + lbr_k::P[k] + cc;
+      n[k] = k < 13 ? (int32_t)(v & LBR_M28) : (int32_t)v;
+      cc = k < 13 ? (v >> 28) : 0;
+    }
+  }
+  for (int it = 0; it < 4; it++) {  // subtract p while v >= p
+    int32_t d[14];
+    int64_t cc = 0;
+    LB_UNROLL for (int k = 0; k < 14; k++) {
+      const int64_t v = (int64_t)n[k] - lbr_k::P[k] + cc;
+      d[k] = k < 13 ? (int32_t)(v & LBR_M28) : (int32_t)v;
+      cc = k < 13 ? (v >> 28) : 0;
+    }
+    if (d[13] < 0) break;
+    LB_UNROLL for (int k = 0; k < 14; k++) n[k] = d[k];
+  }
+  fp r;
+  LB_UNROLL for (int w = 0; w < 12; w++) {
+    const int b = 32 * w, q = b / 28, s = b - 28 * q;
+    uint32_t v = (uint32_t)n[q] >> s;
+    if (q + 1 < 14) v |= (uint32_t)n[q + 1] << (28 - s);
+    if (s > 24 && q + 2 < 14) v |= (uint32_t)n[q + 2] << (56 - s);
+    r.v[w] = v;
+  }
+  return r;
+}
+// slots src .. src + n - 1 -> 2^384-Montgomery words in staging (R' -> R: one row product by
+// 2^384 mod p), canonical on lane e's read (r_fp_of)
+__device__ __forceinline__ void r_export(int32_t* S_generic, int src, int n) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb();
+  for (int e = r_row(); e < n; e += LBR_NROWS) {
+    const int y = S[16 * (src + e) + k];
+    S[16 * (LBR_XS + e) + k] = rp_mul(r_cx_const<14>{lbr_k::K_EXPORT}, y, k);
+  }
+  r_sync();
+}
+__device__ __forceinline__ fp r_fp_of_staged(int32_t* S_generic, int e) {
+  lds_i32* S = r_lds(S_generic);
+  int32_t l[14];
+  LB_UNROLL for (int k = 0; k < 14; k++) l[k] = S[16 * (LBR_XS + e) + k];
+  return r_canon(l);
+}
+
+// Fp12 element e of a word-major SoA array (n elements) <-> an area
+__device__ __forceinline__ void r_load_soa12(int32_t* S, int dst, const uint32_t* base, uint32_t n, uint32_t e) {
+  const int t = r_tid();
+  if (t < 12) {
+    fp v;
+    for (int w = 0; w < 12; w++) v.v[w] = base[(size_t)(12 * t + w) * n + e];
+    r_stage_fp(S, t, v);
+  }
+  r_sync();
+  r_import_staged(S, dst, 12);
+}
+__device__ __forceinline__ void r_store_soa12(int32_t* S, int src, uint32_t* base, uint32_t n, uint32_t e) {
+  r_export(S, src, 12);
+  const int t = r_tid();
+  if (t < 12) {
+    const fp v = r_fp_of_staged(S, t);
+    for (int w = 0; w < 12; w++) base[(size_t)(12 * t + w) * n + e] = v.v[w];
+  }
+  r_sync();
+}
+// n (<= 16) elements given by lane 0 in `vals` (shared memory) -> slots dst ..
+__device__ __forceinline__ void r_import_fps(int32_t* S, int dst, const fp* vals, int n) {
+  const int t = r_tid();
+  if (t < n) r_stage_fp(S, t, vals[t]);
+  r_sync();
+  r_import_staged(S, dst, n);
+}
+
+// ---------------------------------------------------------------- program loading
+__device__ void r_init(int32_t* S_generic, int nprog = LBR_PROGS_FE, int first = 0) {
+  lds_i32* S = r_lds(S_generic);
+  const int t = r_tid();
+  {
+    lds_i32x4* dst = (lds_i32x4*)(S + LBR_SLOT_WORDS + LBR_MISC);
+    const i32x4* src = reinterpret_cast<const i32x4*>(LBR_PROGS + first);
+    for (int i = t; i < nprog / 4; i += LBR_NT) dst[i] = src[i];
+    if (t == 0) S[LBR_SLOT_WORDS + 0] = first;
+  }
+  for (int i = t; i < LBR_N_CONST * 16; i += LBR_NT) S[16 * LBR_CONST + i] = LBR_CONST_LIMBS[i >> 4][i & 15];
+  r_sync();
+}
+
+// ---------------------------------------------------------------- Fp12 ops on 12-slot areas
+__device__ void r_mul(int32_t* S, int dst, int a, int b) {
+  r_gather(S, LBR_IN, 24, [&](int e) { return e < 12 ? a + e : b + e - 12; });
+  r_exec(S, LBR_MUL12);
+  r_out(S, LBR_MUL12, 0, 12, dst);
+}
+__device__ void r_sqr(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 12);
+  r_exec(S, LBR_SQR12);
+  r_out(S, LBR_SQR12, 0, 12, dst);
+}
+// a^2 for a in the cyclotomic subgroup (Granger-Scott: 18 products instead of 36)
+__device__ void r_csqr(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 12);
+  r_exec(S, LBR_CSQR12);
+  r_out(S, LBR_CSQR12, 0, 12, dst);
+}
+__device__ void r_frob(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 12);
+  r_exec(S, LBR_FROB);
+  r_out(S, LBR_FROB, 0, 12, dst);
+}
+__device__ void r_frob2(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 12);
+  r_exec(S, LBR_FROB2);
+  r_out(S, LBR_FROB2, 0, 12, dst);
+}
+// 1 if area a is 1 (exact: canonical words compared)
+__device__ bool r_is_one(int32_t* S_generic, int a) {
+  lds_i32* S = r_lds(S_generic);
+  r_export(S_generic, a, 12);
+  const int t = r_tid();
+  if (t == 0) S[LBR_SLOT_WORDS + 1] = 0;
+  r_sync();
+  if (t < 12) {
+    const fp v = r_fp_of_staged(S_generic, t);
+    const fp want = t == 0 ? fp_one() : fp_zero();
+    if (!fp_eq(v, want)) atomicOr((int*)&S_generic[LBR_SLOT_WORDS + 1], 1);
+  }
+  r_sync();
+  const int r = S[LBR_SLOT_WORDS + 1];
+  r_sync();
+  return r == 0;
+}
+// areas a and b equal (canonical comparison)
+__device__ bool r_eq(int32_t* S_generic, int a, int b) {
+  lds_i32* S = r_lds(S_generic);
+  __shared__ fp va[12];
+  r_export(S_generic, a, 12);
+  const int t = r_tid();
+  if (t < 12) va[t] = r_fp_of_staged(S_generic, t);
+  if (t == 0) S[LBR_SLOT_WORDS + 1] = 0;
+  r_sync();
+  r_export(S_generic, b, 12);
+  if (t < 12 && !fp_eq(va[t], r_fp_of_staged(S_generic, t))) atomicOr((int*)&S_generic[LBR_SLOT_WORDS + 1], 1);
+  r_sync();
+  const int r = S[LBR_SLOT_WORDS + 1];
+  r_sync();
+  return r == 0;
+}
+// dst = a^-1 by norms down to Fp2 (lb_wave.h w_inv): one Fp inversion on thread 0 (inline EEA)
+__device__ void r_inv(int32_t* S, int dst, int a, int t1, int t2, int t3) {
+  __shared__ fp nv[2];
+  r_conj(S, t1, a);     // X
+  r_mul(S, t2, a, t1);  // t
+  r_frob2(S, t3, t2);   // t^(p^2)
+  r_frob2(S, dst, t3);  // t^(p^4)
+  r_mul(S, t3, t3, dst);  // u
+  r_mul(S, t2, t2, t3);   // n = t u (slots 0, 1)
+  r_export(S, t2, 2);
+  if (r_tid() == 0) {
+    const fp n0 = r_fp_of_staged(S, 0), n1 = r_fp_of_staged(S, 1);
+    const fp ni = fp_inv_i(fp_add(fp_sqr(n0), fp_sqr(n1)));
+    nv[0] = fp_mul(n0, ni);
+    nv[1] = fp_neg(fp_mul(n1, ni));
+  }
+  r_sync();
+  r_import_fps(S, t2, nv, 2);  // slots 2..11 of t2 are zero (n lies in Fp2)
+  r_mul(S, t3, t3, t2);  // t^-1
+  r_mul(S, dst, t1, t3);
+}
+// dst = a^|x| for a in the cyclotomic subgroup (a must not alias dst)
+__device__ void r_pow_xabs(int32_t* S, int dst, int a) {
+  r_copy(S, dst, a, 12);
+  for (int i = 62; i >= 0; i--) {
+    r_csqr(S, dst, dst);
+    if ((LB_X_ABS >> i) & 1ull) r_mul(S, dst, dst, a);
+  }
+}
+// f^(3 (p^12 - 1) / r), the chain of lb_pairing.h final_exponentiation (areas 1..6); after the
+// easy part every value lies in the cyclotomic subgroup, so the squarings are r_csqr
+__device__ void r_final_exp(int32_t* S, int dst, int f) {
+  const int T0 = LBR_A(1), A0 = LBR_A(2), B0 = LBR_A(3), C0 = LBR_A(4), X0 = LBR_A(5), Y0 = LBR_A(6);
+  r_inv(S, Y0, f, A0, B0, C0);
+  r_conj(S, X0, f);
+  r_mul(S, T0, X0, Y0);
+  r_frob2(S, X0, T0);
+  r_mul(S, T0, X0, T0);
+  r_pow_xabs(S, X0, T0);
+  r_mul(S, X0, X0, T0);
+  r_conj(S, A0, X0);
+  r_pow_xabs(S, X0, A0);
+  r_mul(S, X0, X0, A0);
+  r_conj(S, A0, X0);
+  r_pow_xabs(S, X0, A0);
+  r_conj(S, X0, X0);
+  r_frob(S, Y0, A0);
+  r_mul(S, B0, X0, Y0);
+  r_pow_xabs(S, X0, B0);
+  r_pow_xabs(S, C0, X0);
+  r_frob2(S, X0, B0);
+  r_mul(S, C0, C0, X0);
+  r_conj(S, X0, B0);
+  r_mul(S, C0, C0, X0);
+  r_csqr(S, X0, T0);
+  r_mul(S, X0, X0, T0);
+  r_mul(S, dst, C0, X0);
+}
+// Miller loop f_{|x|,Q}(P), conjugated, into area dst; P at LBR_PT (xP, yP), Q at LBR_PT + 2
+// (xq.c0, xq.c1, yq.c0, yq.c1); T at LBR_PT + 6..11.  Same steps as lb_wave.h w_miller.
+__device__ void r_miller(int32_t* S_generic, int dst) {
+  lds_i32* S = r_lds(S_generic);
+  const int PP = LBR_PT, QQ = LBR_PT + 2, TT = LBR_PT + 6;
+  r_set_one(S_generic, dst);
+  {
+    const int t = r_tid();
+    if (t < 6 * 16) {
+      const int e = t >> 4, k = t & 15;
+      int v;
+      if (e < 4) v = S[16 * (QQ + e) + k];
+      else if (e == 4) {
+        v = 0;
+        LB_UNROLL for (int i = 0; i < 14; i++) v = k == i ? lbr_k::ONE[i] : v;
+      } else v = 0;
+      S[16 * (TT + e) + k] = v;
+    }
+    r_sync();
+  }
+  for (int i = 62; i >= 0; i--) {
+    r_gather(S_generic, LBR_IN, 20, [&](int e) { return e < 12 ? dst + e : (e < 18 ? TT + e - 12 : PP + e - 18); });
+    r_exec(S_generic, LBR_DBL_STEP);
+    r_out(S_generic, LBR_DBL_STEP, 0, 12, dst);
+    r_out(S_generic, LBR_DBL_STEP, 12, 6, TT);
+    if ((LB_X_ABS >> i) & 1ull) {
+      r_gather(S_generic, LBR_IN, 24, [&](int e) {
+        return e < 12 ? dst + e : (e < 18 ? TT + e - 12 : (e < 22 ? QQ + e - 18 : PP + e - 22));
+      });
+      r_exec(S_generic, LBR_ADD_STEP);
+      r_out(S_generic, LBR_ADD_STEP, 0, 12, dst);
+      r_out(S_generic, LBR_ADD_STEP, 12, 6, TT);
+    }
+  }
+  r_conj(S_generic, dst, dst);
+}

@@ -30,7 +30,7 @@ GROUPS = {
     1: ["k_sig_subgroup", "k_sig_subgroup_g8", "k_sig_agg_chunks", "k_sig_agg_groups"],
     2: ["k_hash_map", "k_sk_to_pk", "k_sign", "k_ssz_zero_hashes", "k_merkleize"],
     3: ["k_hash_finish"],
-    4: ["k_miller_lane", "k_pk_chunks", "k_pk_chunks_idx", "k_pk_blind", "k_gsum_chunks", "k_gsum_final"],
+    4: ["k_miller_lane", "k_pk_chunks", "k_pk_chunks_idx", "k_pk_blind", "k_gsum_chunks", "k_gsum_tree", "k_gsum_final"],
     5: ["k_miller_wave", "k_tree_up_U", "k_ml_S", "k_root_check", "k_root_partial", "k_partials_check", "k_search_ml",
         "k_search_fe", "k_search_match", "k_miller_g8", "k_kzg_check"],
     6: ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
@@ -39,6 +39,7 @@ GROUPS = {
         "k_kzg_setup_g1", "k_kzg_setup_g2"],
     8: ["k_hash_finish_g8"],
     9: ["k_msm_buckets_g8", "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind_g8", "k_sig_blind", "k_g2_sum64"],
+    10: ["k_miller_row", "k_tree_up_row"],
 }
 N_GROUPS = len(GROUPS)
 GROUP_OF = {k: g for g, ks in GROUPS.items() for k in ks}

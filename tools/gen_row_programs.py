@@ -15,7 +15,8 @@ them from the tower formulas) keep their slot map and phase schedule; only the e
   pair      (slot & 0xffff) | (coef << 16), coef a signed 16-bit integer; padding: the zero slot,
             coefficient 0
   flags     bit 0: every task's x operand is one slot with coefficient 1 (read as is, no
-            reduction); bit 1: the same for y
+            reduction); bit 1: the same for y; bit 2: some x operand has a coefficient sum above
+            16 (the quotient reduction runs; otherwise only the limb carries); bit 3: the same for y
 
 Arithmetic (mirrored exactly by RowModel below and checked against big integers and the oracle):
 a slot value v is an integer in (-2p, 2p) congruent to the element times R' (mod p); an operand
@@ -147,6 +148,62 @@ def from_row(l):
     return val(l) * pow(RP, -1, P) % P
 
 
+# ------------------------------------------------------------ programs
+class RowProg(G.Prog):
+    """(A/B: ROW_PLAIN=1) every product operand one slot with coefficient 1: sums materialised by a
+    linear task first.  Measured slower than operand sums inside the product phase (one phase
+    more per operation), so the default keeps the wave programs' operand sums."""
+
+    def mul(self, x, y):
+        if os.environ.get("ROW_PLAIN") == "1":
+            return super().mul(self.mat(x), self.mat(y))
+        return super().mul(x, y)
+
+
+def f4sqr(t, a0, a1):
+    """(a0 + a1 s)^2 in Fp4 = Fp2[s]/(s^2 - xi): (a0^2 + xi a1^2, (a0 + a1)^2 - a0^2 - a1^2)"""
+    t0 = t.f2sqr(a0)
+    t1 = t.f2sqr(a1)
+    r0 = t.f2add(t.f2xi(t1), t0)
+    r1 = t.f2sub(t.f2sub(t.f2sqr(t.f2add(a0, a1)), t0), t1)
+    return r0, r1
+
+
+def cyclotomic_sqr(t, a):
+    """Granger-Scott squaring of an element of the cyclotomic subgroup (the final exponentiation's
+    hard part): three Fp4 squarings, 18 Fp products in one phase instead of SQR12's 36"""
+    (a00, a01, a02), (a10, a11, a12) = a
+    t0 = f4sqr(t, a00, a11)
+    t1 = f4sqr(t, a10, a02)
+    t2 = f4sqr(t, a01, a12)
+
+    def lin3m2(x, y, sign):  # 3 x -/+ 2 y
+        return (x[0].scale(3) + y[0].scale(2 * sign), x[1].scale(3) + y[1].scale(2 * sign))
+    r00 = lin3m2(t0[0], a00, -1)
+    r01 = lin3m2(t1[0], a01, -1)
+    r02 = lin3m2(t2[0], a02, -1)
+    r10 = lin3m2(t.f2xi(t2[1]), a10, 1)
+    r11 = lin3m2(t0[1], a11, 1)
+    r12 = lin3m2(t1[1], a12, 1)
+    return (r00, r01, r02), (r10, r11, r12)
+
+
+def build_programs():
+    """the wave programs' formulas (tools/gen_wave_programs.py build_programs) traced into
+    RowProg, plus CSQR12"""
+    saved = G.Prog
+    G.Prog = RowProg
+    try:
+        progs = G.build_programs()
+        pg = RowProg("CSQR12")
+        t = G.T(pg)
+        pg.output(G.fp12_flat(cyclotomic_sqr(t, G.fp12_in(pg, 0))))
+        progs["CSQR12"] = pg
+    finally:
+        G.Prog = saved
+    return progs
+
+
 # ------------------------------------------------------------ encoding
 class RowCode:
     def __init__(self, words, n_prods, n_lins, n_phases, ntemp):
@@ -180,11 +237,17 @@ def encode(pg):
     def plain(lins):
         return all(len(l.d) == 1 and list(l.d.values())[0] == 1 for l in lins)
 
+    def reduce(lins):
+        # an operand of slot values |v| < 2p with sum |c| <= 16 stays below 32 p < 2^386: its
+        # product is below 1.4 p without the quotient reduction (only the limb carries run)
+        return any(sum(abs(c) for c in l.d.values()) > 16 for l in lins)
+
     for kind, tasks in phases:
         if kind == 0:
             xs, ys = [t[2] for t in tasks], [t[3] for t in tasks]
             nx, ny = max(len(x.d) for x in xs), max(len(y.d) for y in ys)
             flags = (1 if plain(xs) else 0) | (2 if plain(ys) else 0)
+            flags |= (4 if reduce(xs) else 0) | (8 if reduce(ys) else 0)
             out += [kind | (flags << 8) | (len(tasks) << 16), nx | (ny << 16)]
             for t in tasks:
                 out += [t[1]] + pairs(t[2], nx) + pairs(t[3], ny)
@@ -204,7 +267,7 @@ def run_row(words, slots):
     pos = 2 + n_out
     S = dict(slots)
 
-    def operand(ps, is_plain):
+    def operand(ps, is_plain, red=True):
         terms = []
         for w in ps:
             slot, coef = w & 0xFFFF, (w >> 16) - ((w >> 16) & 0x8000) * 2
@@ -212,7 +275,7 @@ def run_row(words, slots):
         if is_plain:
             assert len(terms) == 1 and terms[0][0] == 1
             return terms[0][1]
-        return lin(terms)
+        return lin(terms, reduce=red)
 
     for _ in range(n_ph):
         h0, h1 = words[pos], words[pos + 1]
@@ -224,8 +287,8 @@ def run_row(words, slots):
         for k in range(n):
             rec = words[pos + k * rs: pos + (k + 1) * rs]
             if kind == 0:
-                x = operand(rec[1:1 + nx], flags & 1)
-                y = operand(rec[1 + nx:1 + nx + ny], flags & 2)
+                x = operand(rec[1:1 + nx], flags & 1, flags & 4)
+                y = operand(rec[1 + nx:1 + nx + ny], flags & 2, flags & 8)
                 new[rec[0]] = rp_mul(x, y)
             else:
                 new[rec[0]] = operand(rec[1:1 + nx], False)
@@ -277,6 +340,18 @@ def _checks(codes):
         assert f12(got) == o.f12_pow(f12(a), P), "FROB"
         got = [from_row(v) for v in run_row(codes["FROB2"].words, S)]
         assert f12(got) == o.f12_pow(f12(a), P * P), "FROB2"
+    # CSQR12 on an element of the cyclotomic subgroup: f^((p^6 - 1)(p^2 + 1))
+    for _ in range(2):
+        a = [rnd.randrange(P) for _ in range(12)]
+        fa = f12(a)
+        g = o.f12_mul(o.f12_conj(fa), o.f12_inv(fa))
+        g = o.f12_mul(o.f12_pow(g, P * P), g)
+        flat = [e for six in g for two in six for e in two]  # tower order
+        assert f12(flat) == g
+        S = dict(base)
+        S.update({G.IN_BASE + k: to_row(flat[k]) for k in range(12)})
+        got = [from_row(v) for v in run_row(codes["CSQR12"].words, S)]
+        assert f12(got) == o.f12_sqr(g), "CSQR12"
     # a few Miller steps against the lone-lane programs' interpreter (values, not limbs)
     Pp = o.sk_to_pk(0x1234567)
     Qq = o.hash_to_g2(b"\x07" * 32)
@@ -289,11 +364,11 @@ def _checks(codes):
         got = [from_row(v) for v in run_row(codes[name].words, S)]
         Sw = {G.CONST_BASE + k: v for k, v in enumerate(cv)}
         Sw.update({G.IN_BASE + k: v for k, v in enumerate(vals)})
-        want = G.run_encoded(G.build_programs()[name].encode(), Sw)
+        want = G.run_encoded(G.build_programs()[name].encode(), Sw)  # the wave programs' own values
         assert got == want, name
 
 
-ORDER = ["MUL12", "SQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP"]
+ORDER = ["MUL12", "SQR12", "CSQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP"]
 
 
 def const_limbs(v):
@@ -301,7 +376,7 @@ def const_limbs(v):
 
 
 def render(check=True):
-    progs = G.build_programs()
+    progs = build_programs()
     codes = {k: encode(v) for k, v in progs.items()}
     if check:
         _checks(codes)
@@ -325,8 +400,9 @@ def render(check=True):
             lines.append(f"#define LBR_PROGS_FE {len(image)}")
     lines.append(f"#define LBR_PROGS_ALL {len(image)}")
     lines.append(f"#define LBR_MAX_TEMPS {maxtemp}")
+    signed = [v - (1 << 32) if v >= (1 << 31) else v for v in image]
     lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_PROGS[{len(image)}] = "
-                 f"{{{', '.join(str(v) for v in image)}}};")
+                 f"{{{', '.join(str(v) for v in signed)}}};")
     # constants: the CONST slots in row form, p, -p^-1 mod 2^392, and the conversion factors
     cv = consts_values()
     rows = [const_limbs(v * RP % P) for v in cv]

@@ -1,0 +1,221 @@
+// Row engine vs wave engine latencies (tools/, not product code): cycles (s_memtime at 100 MHz
+// -> converted by the host with the shader clock it measures with s_memrealtime? no: wall ns
+// from clock64 deltas of the realtime counter) per operation of one workgroup.
+//   tools/ubench/row_bench
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#define LB_KGROUP 99
+__device__ unsigned long long g_ph[64][3];
+__device__ int g_ph_n;
+#define LBR_PHASE_HOOK(ph, kind, n)                                  \
+  if (threadIdx.x == 0 && g_ph_n < 64) {                             \
+    g_ph[g_ph_n][0] = __builtin_readcyclecounter();                  \
+    g_ph[g_ph_n][1] = kind;                                          \
+    g_ph[g_ph_n][2] = n;                                             \
+    g_ph_n++;                                                        \
+  }
+#include "lb_kernels.h"
+
+__device__ __forceinline__ uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+
+// one row: a chain of rp_mul
+__global__ void __launch_bounds__(64) k_rp_chain(int iters, uint64_t* out, int* sink) {
+  const int k = threadIdx.x & 15;
+  int y = k < 13 ? (k * 12345 + 7) & LBR_M28 : (k == 13 ? 1000 : 0);
+  int x[14];
+  for (int i = 0; i < 14; i++) x[i] = (i * 777 + 3) & LBR_M28;
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    y = rp_mul(x, y, k);
+    x[it % 14] ^= y & 1;  // keep x live / varying
+  }
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = y;
+}
+template <int OP>
+__global__ void __launch_bounds__(LBR_NT) k_row_ops(int iters, uint64_t* out) {
+  LBR_SHARED(S);
+  r_init(S);
+  r_set_one(S, LBR_A(0));
+  r_set_one(S, LBR_A(1));
+  r_sync();
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    if (OP == 0) r_sqr(S, LBR_A(0), LBR_A(0));
+    if (OP == 1) r_mul(S, LBR_A(0), LBR_A(0), LBR_A(1));
+    if (OP == 2) r_copy(S, LBR_IN, LBR_A(0), 12);
+    if (OP == 3) r_exec(S, LBR_SQR12);
+    if (OP == 4) r_csqr(S, LBR_A(0), LBR_A(0));
+    if (OP == 5) r_final_exp(S, LBR_A(0), LBR_A(0));
+  }
+  r_sync();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+}
+template <int OP>
+__global__ void __launch_bounds__(LBR_NT) k_phases(unsigned long long* out) {
+  LBR_SHARED(S);
+  r_init(S);
+  r_set_one(S, LBR_A(0));
+  if (threadIdx.x == 0) g_ph_n = 0;
+  r_copy(S, LBR_IN, LBR_A(0), 24);
+  r_sync();
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  if (OP == 0) r_exec(S, LBR_CSQR12);
+  if (OP == 1) r_exec(S, LBR_MUL12);
+  if (OP == 2) r_exec(S, LBR_DBL_STEP);
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  if (threadIdx.x == 0) { out[0] = t0; out[1] = t1; }
+}
+template <int OP>
+__global__ void __launch_bounds__(64) k_wave_ops(int iters, uint64_t* out) {
+  LBW_SHARED(S);
+  w_init_consts(S);
+  w_set_one(S, LBW_A(0));
+  w_set_one(S, LBW_A(1));
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    if (OP == 0) w_sqr(S, LBW_A(0), LBW_A(0));
+    if (OP == 1) w_mul(S, LBW_A(0), LBW_A(0), LBW_A(1));
+  }
+  w_sync();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+}
+
+
+// ---- 32-lane group variant: column g at lane g (0..27), shifts by wave_shr:1
+#define WSHR1 0x138
+template <int TOP>  // TOP < 0: carries out of lane 13 dropped (mod 2^392); else lane TOP keeps whole
+__device__ __forceinline__ int n32(int64_t v, int g) {
+  const int64_t q = v >> 28;
+  int l = (int)(v & LBR_M28);
+  int qlo = (int)(q & LBR_M28), qhi = (int)(q >> 28);
+  if (TOP >= 0) {
+    if (g == TOP - 1) { qlo = (int)q; qhi = 0; }
+    if (g >= TOP) { l = g == TOP ? (int)v : 0; qlo = qhi = 0; }
+  }
+  const int s1 = r_dpp<WSHR1>(qlo), s2 = r_dpp<WSHR1>(r_dpp<WSHR1>(qhi));
+  l += s1 + s2;
+  int c = l >> 28, l2 = l & LBR_M28;
+  if (TOP >= 0 && g >= TOP) { c = 0; l2 = g == TOP ? l : 0; }
+  return l2 + r_dpp<WSHR1>(c);
+}
+template <int I, class XS>
+__device__ __forceinline__ void s32(const XS& x, int yi, int64_t (&a)[2]) {
+  if constexpr (I < 14) {
+    if constexpr (I > 0) yi = r_dpp<WSHR1>(yi);
+    a[I & 1] += (int64_t)x[I] * yi;
+    s32<I + 1>(x, yi, a);
+  }
+}
+template <class XS>
+__device__ __forceinline__ int rp_mul32(const XS& x, int y, int g) {
+  int64_t a[2] = {0, 0};
+  s32<0>(x, y, a);
+  int64_t lo = a[0] + a[1];
+  int t = n32<-1>(lo, g);
+  t = g < 14 ? t : 0;
+  int64_t b[2] = {0, 0};
+  s32<0>(r_cx_pinv{}, t, b);
+  int m = n32<-1>(b[0] + b[1], g);
+  m = g < 14 ? m : 0;
+  a[0] = lo; a[1] = 0;
+  s32<0>(r_cx_p{}, m, a);
+  lo = a[0] + a[1];
+  const int64_t u13 = r_dpp64<LBR_SHR(1)>(lo), u12 = r_dpp64<LBR_SHR(2)>(lo), u11 = r_dpp64<LBR_SHR(3)>(lo);
+  const int64_t E = u13 + (u12 >> 28) + (u11 >> 56);
+  const int64_t C = (E + LBR_M28) >> 28;
+  const int64_t r = g == 14 ? lo + C : ((g > 14 && g < 28) ? lo : 0);
+  return n32<27>(r, g);  // limb g - 14 at lanes 14..27
+}
+__global__ void __launch_bounds__(64) k_rp32_chain(int iters, uint64_t* out, int* sink) {
+  __shared__ int buf[2][32];
+  const int g = threadIdx.x & 31, h = threadIdx.x >> 5;
+  int y = g < 13 ? (g * 12345 + 7) & LBR_M28 : (g == 13 ? 1000 : 0);
+  int x[14];
+  for (int i = 0; i < 14; i++) x[i] = (i * 777 + 3) & LBR_M28;
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    const int r = rp_mul32(x, y, g);
+    // move limbs from lanes 14..27 to 0..13 through LDS (as the engine's slot store + reload)
+    if (g >= 14 && g < 28) buf[h][g - 14] = r;
+    if (g >= 28) buf[h][g - 14] = 0;
+    y = g < 14 ? buf[h][g] : 0;
+    x[it % 14] ^= y & 1;
+  }
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = y;
+}
+// correctness: one product each way, limbs out
+__global__ void k_cmp(const int* xin, const int* yin, int* o16, int* o32) {
+  const int k = threadIdx.x & 15, g = threadIdx.x & 31;
+  int x[14];
+  for (int i = 0; i < 14; i++) x[i] = xin[i];
+  if (threadIdx.x < 16) o16[k] = rp_mul(x, k < 14 ? yin[k] : 0, k);
+  if (threadIdx.x < 32) {
+    const int r = rp_mul32(x, g < 14 ? yin[g] : 0, g);
+    if (g >= 14 && g < 28) o32[g - 14] = r;
+  }
+}
+
+int main() {
+  uint64_t* d;
+  int* sink;
+  hipMalloc(&d, 64);
+  hipMalloc(&sink, 4096);
+  uint64_t h;
+  auto run = [&](const char* name, auto launch, int iters) {
+    launch(iters);  // warm
+    hipDeviceSynchronize();
+    launch(iters);
+    hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+    printf("%-28s %8.3f us per op\n", name, (double)h * 10.0 / 1000.0 / iters);
+  };
+  run("rp_mul chain (1 row)", [&](int n) { hipLaunchKernelGGL(k_rp_chain, dim3(1), dim3(64), 0, 0, n, d, sink); }, 2000);
+  run("rp_mul32 chain (1 group)", [&](int n) { hipLaunchKernelGGL(k_rp32_chain, dim3(1), dim3(64), 0, 0, n, d, sink); }, 2000);
+  {
+    int hx[14], hy[14];
+    for (int i = 0; i < 14; i++) { hx[i] = (i * 7919 + 13) & 0x0fffffff; hy[i] = (i * 104729 + 5) & 0x0fffffff; }
+    hx[13] = 1000; hy[13] = 77777;
+    int *dx, *dy, *o16, *o32;
+    hipMalloc(&dx, 64); hipMalloc(&dy, 64); hipMalloc(&o16, 64); hipMalloc(&o32, 64);
+    hipMemcpy(dx, hx, 56, hipMemcpyHostToDevice); hipMemcpy(dy, hy, 56, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_cmp, dim3(1), dim3(64), 0, 0, dx, dy, o16, o32);
+    int a[14], b[14];
+    hipMemcpy(a, o16, 56, hipMemcpyDeviceToHost); hipMemcpy(b, o32, 56, hipMemcpyDeviceToHost);
+    printf("x:"); for (int i = 0; i < 14; i++) printf(" %d", hx[i]); printf("\ny:"); for (int i = 0; i < 14; i++) printf(" %d", hy[i]);
+    printf("\nr16:"); for (int i = 0; i < 14; i++) printf(" %d", a[i]); printf("\nr32:"); for (int i = 0; i < 14; i++) printf(" %d", b[i]); printf("\n");
+  }
+  run("row SQR12 (1024 thr)", [&](int n) { hipLaunchKernelGGL(k_row_ops<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row MUL12", [&](int n) { hipLaunchKernelGGL(k_row_ops<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row copy12", [&](int n) { hipLaunchKernelGGL(k_row_ops<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row exec SQR12 only", [&](int n) { hipLaunchKernelGGL(k_row_ops<3>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row CSQR12", [&](int n) { hipLaunchKernelGGL(k_row_ops<4>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row final exp", [&](int n) { hipLaunchKernelGGL(k_row_ops<5>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 3);
+  {
+    unsigned long long* dd;
+    hipMalloc(&dd, 64);
+    const char* nm[3] = {"CSQR12", "MUL12", "DBL_STEP"};
+    for (int op = 0; op < 3; op++) {
+      if (op == 0) hipLaunchKernelGGL(k_phases<0>, dim3(1), dim3(LBR_NT), 0, 0, dd);
+      if (op == 1) hipLaunchKernelGGL(k_phases<1>, dim3(1), dim3(LBR_NT), 0, 0, dd);
+      if (op == 2) hipLaunchKernelGGL(k_phases<2>, dim3(1), dim3(LBR_NT), 0, 0, dd);
+      hipDeviceSynchronize();
+      unsigned long long tt[2], ph[64][3];
+      int np;
+      hipMemcpy(tt, dd, 16, hipMemcpyDeviceToHost);
+      hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof(ph));
+      hipMemcpyFromSymbol(&np, HIP_SYMBOL(g_ph_n), 4);
+      printf("%s: %llu cycles total;", nm[op], tt[1] - tt[0]);
+      unsigned long long prev = tt[0];
+      for (int i = 0; i < np; i++) { printf(" %s%llu:%llu", ph[i][1] ? "L" : "P", ph[i][2], ph[i][0] - prev); prev = ph[i][0]; }
+      printf("\n");
+    }
+  }
+  run("wave SQR12 (64 thr)", [&](int n) { hipLaunchKernelGGL(k_wave_ops<0>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
+  run("wave MUL12", [&](int n) { hipLaunchKernelGGL(k_wave_ops<1>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
+  return 0;
+}
