@@ -126,6 +126,11 @@ struct lb_engine {
   dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
       set_live, gacc, gp_aff, gp_inf, chunk_root;
   uint32_t gmax_chunks = 0;  // chunks of the largest root (the k_gsum_tree levels), read back with n_u
+  bool gsum_tree = true;     // LB_GSUM_TREE=0: the chunk sums added serially per root (A/B)
+  // this pipeline run's forms: `alone` (device_alone at its start) picks the latency forms -- the
+  // row engine (row_fe: LB_ROW_FE=0 disables it) and the per-root sum tree over 4-member chunks
+  bool alone = false, row_fe = true;
+  uint32_t gchunk = LB_GROUP_CHUNK;
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
   // parked lone-lane state: k_hash_finish's points (4 x 72 words per launched lane), k_miller_lane's T
@@ -374,6 +379,8 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
   if (const char* rm = getenv("LB_ROW_MAX")) e->row_max = (uint32_t)strtoul(rm, nullptr, 10);
+  if (const char* gt = getenv("LB_GSUM_TREE")) e->gsum_tree = std::atoi(gt) != 0;
+  if (const char* rf = getenv("LB_ROW_FE")) e->row_fe = std::atoi(rf) != 0;
   if (const char* pm = getenv("LB_PRIO_MAX")) e->prio_max = (uint32_t)strtoul(pm, nullptr, 10);
   if (const char* ml = getenv("LB_MILLER_LDS3_MAX")) e->miller_lds3_max = (uint32_t)strtoul(ml, nullptr, 10);
   if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
@@ -743,22 +750,24 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
   {
     stage_scope sc(e, ST_GSUM, s1);
     // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
-    const uint32_t nch = nuh + n / LB_GROUP_CHUNK;
+    const uint32_t nch = nuh + n / e->gchunk;
     hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu,
                        e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
                        e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
     // the per-root tree over the chunk sums (levels until one partial per root is left)
-    for (uint32_t st = 1; st < e->gmax_chunks; st *= LB_GSUM_FAN)
+    const bool tree = e->gsum_tree && e->gchunk == LB_GROUP_CHUNK_ALONE;
+    for (uint32_t st = 1; tree && st < e->gmax_chunks; st *= LB_GSUM_FAN)
       hipLaunchKernelGGL(k_gsum_tree, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->chunk_root.as<uint32_t>(), st, e->gacc.as<uint32_t>());
     hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
-                       e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>());
+                       e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(),
+                       tree ? 0u : 1u);
   }
   {
     stage_scope sc(e, ST_MILLER, s1);
     const bool shared = e->miller_form == 1 ||
                         (e->miller_form == 0 && !device_alone(e));
-    if (nuh <= e->row_max) {
+    if (nuh <= e->row_max && e->alone && e->row_fe) {
       hipLaunchKernelGGL(k_miller_row, dim3(nuh), dim3(LBR_NT), 0, s1, n, mu, nu, e->gp_aff.as<uint32_t>(),
                          e->gp_inf.as<uint32_t>(), e->h_aff.as<uint32_t>(), e->treeP.as<uint32_t>());
     } else if (nuh <= e->miller_wave_max) {
@@ -784,7 +793,7 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
   {
     stage_scope sc(e, ST_TREE_P, s1);
     for (uint32_t lo = mu / 2; lo >= 1; lo /= 2) {
-      if (lo <= e->row_max)
+      if (lo <= e->row_max && e->alone && e->row_fe)
         hipLaunchKernelGGL(k_tree_up_row, dim3(lo), dim3(LBR_NT), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
       else
         hipLaunchKernelGGL(k_tree_up_U, dim3(lo), dim3(64), 0, s1, mu, lo, nu, e->treeP.as<uint32_t>());
@@ -799,6 +808,8 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
 static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
   e->partial_serial = 0;
+  e->alone = device_alone(e);
+  e->gchunk = (e->alone && e->gsum_tree) ? LB_GROUP_CHUNK_ALONE : LB_GROUP_CHUNK;
   int st = fill_scalars(e, n, scalars);
   if (st != LB_OK) return st;
   mj = 1;
@@ -923,9 +934,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
                          e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
                          e->gpos.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, (uint32_t)LB_GROUP_CHUNK, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
-                         e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
-                         e->chunk_root.as<uint32_t>(), e->n_u.as<uint32_t>() + 1);
+      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gchunk, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
+                         e->gch.as<uint32_t>(), nullptr, nullptr, nullptr, e->n_u.as<uint32_t>() + 1);
+      hipLaunchKernelGGL(k_chunk_fill, dim3(nblk(n + n / e->gchunk + 1)), dim3(LB_TPB), 0, s1, nu,
+                         e->gchunk, e->goff.as<uint32_t>(), e->gch.as<uint32_t>(),
+                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>());
       hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
       // distinct-root count to the host: the per-root kernels below are launched over it (a
@@ -1030,7 +1043,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
   // ---- s2: ML(-G1, S_root)
   {
     stage_scope sc(e, ST_ML_S, s2);
-    hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(LB_FE_TPB), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
+    if (e->alone && e->row_fe)
+      hipLaunchKernelGGL(k_ml_S_row, dim3(1), dim3(LBR_NT), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(k_ml_S, dim3(1), dim3(64), 0, s2, mj, e->treeS.as<uint32_t>(), e->fS.as<uint32_t>());
   }
   LB_HIP(hipEventRecord(e->ev_s, s2));
   LB_HIP(hipStreamWaitEvent(s1, e->ev_s, 0));  // join
@@ -1667,7 +1683,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   {
     stage_scope sc(e, ST_ROOT, e->stream);
     LB_HIP(e->y_root.ensure(576));
-    hipLaunchKernelGGL(k_root_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL((e->alone && e->row_fe) ? k_root_check_row : k_root_check, dim3(1), dim3((e->alone && e->row_fe) ? LBR_NT : 64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
   }
   LB_HIP(hipGetLastError());
@@ -1712,7 +1728,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
   LB_HIP(e->parts.ensure(576));
   {
     stage_scope sc(e, ST_ROOT, e->stream);
-    hipLaunchKernelGGL(k_root_partial, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(),
+    hipLaunchKernelGGL((e->alone && e->row_fe) ? k_root_partial_row : k_root_partial, dim3(1), dim3((e->alone && e->row_fe) ? LBR_NT : 64), 0, e->stream, mu, e->treeP.as<uint32_t>(),
                        e->fS.as<uint32_t>(), e->parts.as<uint8_t>());
   }
   LB_HIP(hipGetLastError());
@@ -1739,7 +1755,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   LB_HIP(e->verdict.ensure(4));
   LB_HIP(e->y_root.ensure(576));
   // this shard's own root check: a passing shard is done, a failing one searches from it
-  hipLaunchKernelGGL(k_root_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, mu, e->treeP.as<uint32_t>(), e->fS.as<uint32_t>(),
+  hipLaunchKernelGGL((e->alone && e->row_fe) ? k_root_check_row : k_root_check, dim3(1), dim3((e->alone && e->row_fe) ? LBR_NT : 64), 0, e->stream, mu, e->treeP.as<uint32_t>(), e->fS.as<uint32_t>(),
                      e->verdict.as<int32_t>(), e->y_root.as<uint32_t>());
   LB_HIP(hipGetLastError());
   std::vector<int32_t> jst(nj);
@@ -1765,7 +1781,8 @@ extern "C" int32_t lb_fp12_product_is_one(lb_engine* e, const uint8_t* partials5
   LB_HIP(e->parts.ensure((size_t)(n ? n : 1) * 576));
   LB_HIP(e->ok.ensure(4));
   if (n) LB_HIP(hipMemcpyAsync(e->parts.p, partials576, (size_t)n * 576, hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(LB_FE_TPB), 0, e->stream, n, e->parts.as<uint8_t>(),
+  const bool prow = e->row_fe && device_alone(e);
+  hipLaunchKernelGGL(prow ? k_partials_check_row : k_partials_check, dim3(1), dim3(prow ? LBR_NT : 64), 0, e->stream, n, e->parts.as<uint8_t>(),
                      e->ok.as<int32_t>());
   LB_HIP(hipGetLastError());
   LB_HIP(hipMemcpyAsync(ok, e->ok.p, 4, hipMemcpyDeviceToHost, e->stream));

@@ -128,17 +128,12 @@ __device__ __forceinline__ uint32_t lb_tid() { return blockIdx.x * blockDim.x + 
 
 #include "lb_wave.h"
 #include "lb_row.h"
-// LB_ROW_FE=1: the final exponentiations, ML(-G1, S), the small-batch per-root Miller loops and the
-// product tree run on the row engine (lb_row.h, one Fp product per 16-lane row, 4-wave
-// workgroups); 0: the wave engine (lb_wave.h, one product per lane, one wave)
-#ifndef LB_ROW_FE
-#define LB_ROW_FE 1
-#endif
-#if LB_ROW_FE
-#define LB_FE_TPB LBR_NT
-#else
-#define LB_FE_TPB 64
-#endif
+// Row-engine forms (lb_row.h: one Fp product per 16-lane row, one 16-wave workgroup per item) of
+// the final exponentiations, ML(-G1, S), the small-batch per-root Miller loops and the product
+// tree: k_*_row next to the wave-engine kernels (one product per lane, one wave).  The engine runs
+// the row forms only while the device has no other batch in flight (latency): a 16-wave
+// workgroup needs a whole CU, which under load costs the batches in flight ~5 % of the headline
+// (profiles/r5_row_ab.txt).
 #include "lb_group_exec.h"
 #include "lb_group.h"
 #include "lb_ssz.h"
@@ -1027,9 +1022,11 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // slot 0xffffffff), probed from a keyed hash of the root (key from the engine's CSPRNG, so crafted
 // roots cannot be aimed at one probe chain); equality is decided on all 32 bytes.  A slot, once
 // claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
-#ifndef LB_GROUP_CHUNK
-#define LB_GROUP_CHUNK 4  // members summed per lane in k_gsum_chunks (then the k_gsum_tree levels)
-#endif
+// members summed per lane in k_gsum_chunks: 4 with the k_gsum_tree levels for a batch alone on
+// the device (latency), 32 with the chunk sums added per root on one lane under load (the tree's
+// wide launches cost the batches in flight throughput, profiles/r5_row_ab.txt); lb_engine.hip
+#define LB_GROUP_CHUNK_ALONE 4
+#define LB_GROUP_CHUNK 32
 #define LB_GSUM_FAN 4     // partial sums combined per lane and level in k_gsum_tree
 #ifndef LB_MSM_CHUNK
 #ifndef LB_MSM_CHUNK
@@ -1154,12 +1151,15 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     const uint32_t c = cnt[u];
     goff[u] = om;
     gch[u] = oc;
-    for (uint32_t k = 0; k < c; k += chunk) {
-      chunk_beg[oc] = om + k;
-      chunk_end[oc] = om + min(k + chunk, c);
-      if (chunk_root) chunk_root[oc] = u;
-      oc++;
-    }
+    if (chunk_beg)  // (chunk_beg == nullptr: k_chunk_fill writes the chunk ranges, one lane per chunk)
+      for (uint32_t k = 0; k < c; k += chunk) {
+        chunk_beg[oc] = om + k;
+        chunk_end[oc] = om + min(k + chunk, c);
+        if (chunk_root) chunk_root[oc] = u;
+        oc++;
+      }
+    else
+      oc += (c + chunk - 1) / chunk;
     om += c;
   }
   if (t == 1023) {
@@ -1167,6 +1167,31 @@ __global__ void __launch_bounds__(1024) k_msg_scan(const uint32_t* __restrict__ 
     gch[nu] = s_c[1023];
   }
   if (max_chunks && t == 0) *max_chunks = s_x;  // (the atomics completed before the scan's barriers)
+}
+#endif  // LB_KG
+
+// The member range and root of every chunk of the per-root grouping, one lane per chunk (root by
+// binary search over the chunk offsets gch): the serial per-thread chunk loop of k_msg_scan took
+// ~2 ms per 116 736-set batch with 4-member chunks (a thread owning the large roots wrote
+// thousands of chunks), on the s1 path the host waits on.
+#if LB_KG(0)
+__global__ void __launch_bounds__(LB_TPB) k_chunk_fill(const uint32_t* __restrict__ n_u, uint32_t chunk,
+                                                       const uint32_t* __restrict__ goff,
+                                                       const uint32_t* __restrict__ gch,
+                                                       uint32_t* __restrict__ chunk_beg, uint32_t* __restrict__ chunk_end,
+                                                       uint32_t* __restrict__ chunk_root) {
+  const uint32_t c = lb_tid(), nu = *n_u;
+  if (c >= gch[nu]) return;
+  uint32_t lo = 0, hi = nu;  // the last u with gch[u] <= c
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (gch[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t b = goff[lo] + (c - gch[lo]) * chunk;
+  chunk_beg[c] = b;
+  chunk_end[c] = min(b + chunk, goff[lo + 1]);
+  chunk_root[c] = lo;
 }
 #endif  // LB_KG
 
@@ -2200,13 +2225,18 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
                                                            const uint32_t* __restrict__ gch,
                                                            const uint32_t* __restrict__ gacc,
                                                            uint32_t* __restrict__ gp_aff,
-                                                           uint32_t* __restrict__ gp_inf) {
+                                                           uint32_t* __restrict__ gp_inf, uint32_t serial) {
   const uint32_t u = blockIdx.x * LB_INV_TPB + threadIdx.x;
   const uint32_t nu = *n_u;
   if (blockIdx.x * LB_INV_TPB >= nu) return;  // whole block idle (uniform)
   const bool act = u < nu;
   g1j acc = jac_infinity<fp>();
-  if (act) acc = soa_ld<g1j>(gacc, n, gch[u]);
+  if (act) {
+    if (serial)  // (A/B: LB_GSUM_TREE=0) the root's chunk sums added on this lane
+      for (uint32_t c = gch[u]; c < gch[u + 1]; c++) acc = jac_add(acc, soa_ld<g1j>(gacc, n, c));
+    else
+      acc = soa_ld<g1j>(gacc, n, gch[u]);
+  }
   const bool zero = jac_is_inf(acc);
   const fp zi = fp_inv_block(act && !zero ? acc.z : fp_one());
   if (!act) return;
@@ -2304,8 +2334,35 @@ __global__ void __launch_bounds__(LBR_NT) k_tree_up_row(uint32_t m, uint32_t lo,
 // fS = ML(-G1, S_root) (1 if S_root is infinity): the G2 half of the root partial product,
 // computed while the per-set Miller loops still run.  Output: 12 Fp in Montgomery form.
 #if LB_KG(5)
-#if LB_ROW_FE
-__global__ void __launch_bounds__(LBR_NT) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
+__global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
+  LBW_SHARED_ML(S);
+  __shared__ int s_inf;
+  const int lane = threadIdx.x;
+  w_init_consts(S, LBW_PROGS_ALL);
+  if (lane == 0) {
+    g2j Sj = soa_ld<g2j>(treeS, 2 * m, 1);
+    s_inf = jac_is_inf(Sj) ? 1 : 0;
+    if (!s_inf) {
+      g2a a;
+      g2_to_aff_inl(a, Sj);
+      w_st(S, LBW_PT + 0, fp_load(LB_G1X));
+      w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
+      w_st(S, LBW_PT + 2, a.x.c0);
+      w_st(S, LBW_PT + 3, a.x.c1);
+      w_st(S, LBW_PT + 4, a.y.c0);
+      w_st(S, LBW_PT + 5, a.y.c1);
+    }
+  }
+  w_sync();
+  if (s_inf)
+    w_set_one(S, LBW_A(7));
+  else
+    w_miller(S, LBW_A(7));
+  w_store_soa12(S, LBW_A(7), fS, 1, 0);
+}
+#endif  // LB_KG
+#if LB_KG(11)
+__global__ void __launch_bounds__(LBR_NT) k_ml_S_row(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
   LBR_SHARED_MILLER(S);
   __shared__ int s_inf;
   __shared__ fp pv[6];
@@ -2333,54 +2390,11 @@ __global__ void __launch_bounds__(LBR_NT) k_ml_S(uint32_t m, const uint32_t* __r
   }
   r_store_soa12(S, LBR_A(7), fS, 1, 0);
 }
-#else
-__global__ void __launch_bounds__(64) k_ml_S(uint32_t m, const uint32_t* __restrict__ treeS, uint32_t* __restrict__ fS) {
-  LBW_SHARED_ML(S);
-  __shared__ int s_inf;
-  const int lane = threadIdx.x;
-  w_init_consts(S, LBW_PROGS_ALL);
-  if (lane == 0) {
-    g2j Sj = soa_ld<g2j>(treeS, 2 * m, 1);
-    s_inf = jac_is_inf(Sj) ? 1 : 0;
-    if (!s_inf) {
-      g2a a;
-      g2_to_aff_inl(a, Sj);
-      w_st(S, LBW_PT + 0, fp_load(LB_G1X));
-      w_st(S, LBW_PT + 1, fp_load(LB_G1NEGY));
-      w_st(S, LBW_PT + 2, a.x.c0);
-      w_st(S, LBW_PT + 3, a.x.c1);
-      w_st(S, LBW_PT + 4, a.y.c0);
-      w_st(S, LBW_PT + 5, a.y.c1);
-    }
-  }
-  w_sync();
-  if (s_inf)
-    w_set_one(S, LBW_A(7));
-  else
-    w_miller(S, LBW_A(7));
-  w_store_soa12(S, LBW_A(7), fS, 1, 0);
-}
-#endif
 #endif  // LB_KG
 
 // root verdict: FE(P_root * fS) == 1   (Pairing.finalverify over the whole batch)
 // (the FE value y goes to y_out for the invalid-set search)
 #if LB_KG(5)
-#if LB_ROW_FE
-__global__ void __launch_bounds__(LBR_NT) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
-                                                       const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
-                                                       uint32_t* __restrict__ y_out) {
-  LBR_SHARED(S);
-  r_init(S);
-  r_load_soa12(S, LBR_A(0), treeP, 2 * m, 1);
-  r_load_soa12(S, LBR_A(7), fS, 1, 0);
-  r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
-  r_final_exp(S, LBR_A(0), LBR_A(0));
-  const bool one = r_is_one(S, LBR_A(0));
-  r_store_soa12(S, LBR_A(0), y_out, 1, 0);
-  if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
-}
-#else
 __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* __restrict__ treeP,
                                                    const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
                                                    uint32_t* __restrict__ y_out) {
@@ -2394,23 +2408,25 @@ __global__ void __launch_bounds__(64) k_root_check(uint32_t m, const uint32_t* _
   w_store_soa12(S, LBW_A(0), y_out, 1, 0);
   if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
-#endif
 #endif  // LB_KG
-
-// root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
-#if LB_KG(5)
-#if LB_ROW_FE
-__global__ void __launch_bounds__(LBR_NT) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
-                                                         const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
+#if LB_KG(11)
+__global__ void __launch_bounds__(LBR_NT) k_root_check_row(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                       const uint32_t* __restrict__ fS, int32_t* __restrict__ verdict,
+                                                       uint32_t* __restrict__ y_out) {
   LBR_SHARED(S);
   r_init(S);
   r_load_soa12(S, LBR_A(0), treeP, 2 * m, 1);
   r_load_soa12(S, LBR_A(7), fS, 1, 0);
   r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
-  r_export(S, LBR_A(0), 12);
-  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(r_fp_of_staged(S, threadIdx.x)));
+  r_final_exp(S, LBR_A(0), LBR_A(0));
+  const bool one = r_is_one(S, LBR_A(0));
+  r_store_soa12(S, LBR_A(0), y_out, 1, 0);
+  if (threadIdx.x == 0) verdict[0] = one ? 1 : 0;
 }
-#else
+#endif  // LB_KG
+
+// root partial product P_root * fS as 576 bytes (multi-GPU exchange format)
+#if LB_KG(5)
 __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t* __restrict__ treeP,
                                                      const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
   LBW_SHARED(S);
@@ -2420,34 +2436,21 @@ __global__ void __launch_bounds__(64) k_root_partial(uint32_t m, const uint32_t*
   w_mul(S, LBW_A(0), LBW_A(0), LBW_A(7));
   if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(w_ld(S, LBW_A(0) + threadIdx.x)));
 }
-#endif
+#endif  // LB_KG
+#if LB_KG(11)
+__global__ void __launch_bounds__(LBR_NT) k_root_partial_row(uint32_t m, const uint32_t* __restrict__ treeP,
+                                                         const uint32_t* __restrict__ fS, uint8_t* __restrict__ out576) {
+  LBR_SHARED(S);
+  r_init(S);
+  r_load_soa12(S, LBR_A(0), treeP, 2 * m, 1);
+  r_load_soa12(S, LBR_A(7), fS, 1, 0);
+  r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
+  r_export(S, LBR_A(0), 12);
+  if (threadIdx.x < 12) fp_plain_to_be48(out576 + 48 * threadIdx.x, fp_from_mont(r_fp_of_staged(S, threadIdx.x)));
+}
 #endif  // LB_KG
 
 #if LB_KG(5)
-#if LB_ROW_FE
-__global__ void __launch_bounds__(LBR_NT) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
-                                                           int32_t* __restrict__ ok) {
-  LBR_SHARED(S);
-  __shared__ int bad;
-  const int t = threadIdx.x;
-  if (t == 0) bad = 0;
-  r_init(S);
-  r_set_one(S, LBR_A(0));
-  for (uint32_t i = 0; i < n; i++) {
-    if (t < 12) {
-      fp x;
-      if (!fp_plain_from_be48(x, parts + (size_t)576 * i + 48 * t, 0xff)) atomicOr(&bad, 1);
-      r_stage_fp(S, t, fp_to_mont(x));
-    }
-    r_sync();
-    r_import_staged(S, LBR_A(7), 12);
-    r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
-  }
-  r_final_exp(S, LBR_A(0), LBR_A(0));
-  const bool one = r_is_one(S, LBR_A(0));
-  if (t == 0) *ok = (one && !bad) ? 1 : 0;
-}
-#else
 __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t* __restrict__ parts,
                                                        int32_t* __restrict__ ok) {
   LBW_SHARED(S);
@@ -2469,7 +2472,30 @@ __global__ void __launch_bounds__(64) k_partials_check(uint32_t n, const uint8_t
   bool one = w_is_one(S, LBW_A(0));
   if (lane == 0) *ok = (one && !bad) ? 1 : 0;
 }
-#endif
+#endif  // LB_KG
+#if LB_KG(11)
+__global__ void __launch_bounds__(LBR_NT) k_partials_check_row(uint32_t n, const uint8_t* __restrict__ parts,
+                                                           int32_t* __restrict__ ok) {
+  LBR_SHARED(S);
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  r_init(S);
+  r_set_one(S, LBR_A(0));
+  for (uint32_t i = 0; i < n; i++) {
+    if (t < 12) {
+      fp x;
+      if (!fp_plain_from_be48(x, parts + (size_t)576 * i + 48 * t, 0xff)) atomicOr(&bad, 1);
+      r_stage_fp(S, t, fp_to_mont(x));
+    }
+    r_sync();
+    r_import_staged(S, LBR_A(7), 12);
+    r_mul(S, LBR_A(0), LBR_A(0), LBR_A(7));
+  }
+  r_final_exp(S, LBR_A(0), LBR_A(0));
+  const bool one = r_is_one(S, LBR_A(0));
+  if (t == 0) *ok = (one && !bad) ? 1 : 0;
+}
 #endif  // LB_KG
 
 // ---------------------------------------------------------------- pubkey aggregation only

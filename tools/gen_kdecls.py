@@ -25,7 +25,7 @@ OUT = os.path.join(CSRC, "lb_kdecl.h")
 # decode kernels are the slow ones)
 GROUPS = {
     0: ["k_decompress_sigs", "k_table_fill", "k_g1_decompress", "k_aggregate", "k_msg_insert", "k_msg_uid_input",
-        "k_msg_uid", "k_msg_count", "k_msg_scan", "k_msg_scatter", "k_job_status", "k_spec_live", "k_live_mismatch",
+        "k_msg_uid", "k_msg_count", "k_msg_scan", "k_chunk_fill", "k_msg_scatter", "k_job_status", "k_spec_live", "k_live_mismatch",
         "k_set_one", "k_g2_set_inf"],
     1: ["k_sig_subgroup", "k_sig_subgroup_g8", "k_sig_agg_chunks", "k_sig_agg_groups"],
     2: ["k_hash_map", "k_sk_to_pk", "k_sign", "k_ssz_zero_hashes", "k_merkleize"],
@@ -40,6 +40,7 @@ GROUPS = {
     8: ["k_hash_finish_g8"],
     9: ["k_msm_buckets_g8", "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind_g8", "k_sig_blind", "k_g2_sum64"],
     10: ["k_miller_row", "k_tree_up_row"],
+    11: ["k_ml_S_row", "k_root_check_row", "k_root_partial_row", "k_partials_check_row"],
 }
 N_GROUPS = len(GROUPS)
 GROUP_OF = {k: g for g, ks in GROUPS.items() for k in ks}
