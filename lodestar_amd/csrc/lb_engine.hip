@@ -111,12 +111,12 @@ struct lb_engine {
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
   hipStream_t stream3 = nullptr;  // s3: pubkey aggregation + blinding, beside the signature decode
-  // batches of at most prio_max sets (a gossip block's proposer check, verifyOnMainThread, a
-  // light-client update) run on a second stream trio created at the device's greatest priority,
-  // so their kernels are not queued behind the bulk batches of the other engines
-  // (main_thread_1set_ms_under_load); created on first use.  LB_PRIO_MAX (0: off)
+  // LB_PRIO_MAX=k: batches of at most k sets run on a second stream trio created at the device's
+  // greatest priority (created on first use).  Off by default: measured through the JS drop-in,
+  // verifyOnMainThread under a gossip load took 396-758 ms with it against 9.0-9.2 ms without,
+  // and the pool's throughput fell 3-5x (profiles/r5_prio_streams_ab.txt)
   hipStream_t hp[3] = {nullptr, nullptr, nullptr};
-  uint32_t prio_max = 32;
+  uint32_t prio_max = 0;
   hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr, ev_pk = nullptr;
   std::mutex mu;
   // workspace
