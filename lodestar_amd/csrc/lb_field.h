@@ -631,10 +631,173 @@ LB_HD fp fp_inv_plain_vt_i(fp a) {
     }
   }
 }
-LB_NI fp fp_inv_plain_vt(fp a) { return fp_inv_plain_vt_i(a); }
+// ---- Bernstein-Yang "safegcd" inversion, variable time (jumps of 62 divsteps on the low 64 bits,
+// then 2x2 transition matrices applied to the full-width values; the divstep loop and the
+// update steps follow the structure of libsecp256k1's modinv64_var, written here for a 381-bit
+// modulus in 7 signed 62-bit limbs).  ~12 jumps for a random input against the binary extended
+// Euclid's ~760 word-array iterations: an inversion on a lone lane 184 us -> ~25 us
+// (tools/ubench/row_bench.hip), on the critical path of every small batch (the final
+// exponentiation's norm, each block's batched inversion in k_hash_finish / k_gsum_final /
+// k_pk_blind, ML(-G1, S)'s affine S).  Public inputs only, so variable time is fine.
+struct lb_s62 {
+  int64_t v[7];
+};
+#define LB_S62_M 0x3fffffffffffffffLL
+LB_HD lb_s62 lb_s62_p() {
+  return lb_s62{{0x39feffffffffaaabLL, 0x3aaffffac54ffffeLL, 0x330d2a0f6b0f6241LL, 0x1dd2e13ce144afd9LL,
+                 0x1ba7b6434bacd764LL, 0x0447a8e5ff9a692cLL, 0x1a0LL}};
+}
+#define LB_S62_PINV 0x360c000300030003ULL  // p^-1 mod 2^62
+LB_HD int lb_ctz64(uint64_t x) { return __builtin_ctzll(x); }
+// 62 divsteps on the low bits of f, g (f odd); returns the new eta, the matrix in t[4] = u, v, q, r
+LB_HD int64_t lb_divsteps62(int64_t eta, uint64_t f0, uint64_t g0, int64_t t[4]) {
+  uint64_t u = 1, v = 0, q = 0, r = 1, f = f0, g = g0, m, w;
+  int i = 62;
+  for (;;) {
+    const int zeros = lb_ctz64(g | (~0ULL << i));  // sentinel at bit i
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    int limit;
+    if (eta < 0) {  // swap with negation: (f, g) <- (g, -f)
+      uint64_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = (uint64_t)0 - tmp;
+      tmp = u; u = q; q = (uint64_t)0 - tmp;
+      tmp = v; v = r; r = (uint64_t)0 - tmp;
+      limit = (int)eta + 1 > i ? i : (int)eta + 1;
+      m = (~0ULL >> (64 - limit)) & 63u;
+      w = (f * g * (f * f - 2)) & m;  // cancels up to 6 low bits of g
+    } else {
+      limit = (int)eta + 1 > i ? i : (int)eta + 1;
+      m = (~0ULL >> (64 - limit)) & 15u;
+      w = f + (((f + 1) & 4) << 1);
+      w = ((uint64_t)0 - w * g) & m;  // up to 4 bits
+    }
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t[0] = (int64_t)u;
+  t[1] = (int64_t)v;
+  t[2] = (int64_t)q;
+  t[3] = (int64_t)r;
+  return eta;
+}
+// (f, g) <- (u f + v g, q f + r g) / 2^62 (exact)
+LB_HD void lb_s62_update_fg(lb_s62& f, lb_s62& g, const int64_t t[4]) {
+  const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+  __int128 cf = (__int128)u * f.v[0] + (__int128)v * g.v[0];
+  __int128 cg = (__int128)q * f.v[0] + (__int128)r * g.v[0];
+  cf >>= 62;
+  cg >>= 62;
+  LB_UNROLL for (int i = 1; i < 7; i++) {
+    cf += (__int128)u * f.v[i] + (__int128)v * g.v[i];
+    cg += (__int128)q * f.v[i] + (__int128)r * g.v[i];
+    f.v[i - 1] = (int64_t)cf & LB_S62_M;
+    cf >>= 62;
+    g.v[i - 1] = (int64_t)cg & LB_S62_M;
+    cg >>= 62;
+  }
+  f.v[6] = (int64_t)cf;
+  g.v[6] = (int64_t)cg;
+}
+// (d, e) <- (u d + v e, q d + r e) / 2^62 mod p, kept in (-2p, p)
+LB_HD void lb_s62_update_de(lb_s62& d, lb_s62& e, const int64_t t[4]) {
+  const lb_s62 M = lb_s62_p();
+  const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+  const int64_t sd = d.v[6] >> 63, se = e.v[6] >> 63;
+  int64_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+  __int128 cd = (__int128)u * d.v[0] + (__int128)v * e.v[0];
+  __int128 ce = (__int128)q * d.v[0] + (__int128)r * e.v[0];
+  md -= (int64_t)((LB_S62_PINV * (uint64_t)cd + (uint64_t)md) & (uint64_t)LB_S62_M);
+  me -= (int64_t)((LB_S62_PINV * (uint64_t)ce + (uint64_t)me) & (uint64_t)LB_S62_M);
+  cd += (__int128)M.v[0] * md;
+  ce += (__int128)M.v[0] * me;
+  cd >>= 62;
+  ce >>= 62;
+  LB_UNROLL for (int i = 1; i < 7; i++) {
+    cd += (__int128)u * d.v[i] + (__int128)v * e.v[i] + (__int128)M.v[i] * md;
+    ce += (__int128)q * d.v[i] + (__int128)r * e.v[i] + (__int128)M.v[i] * me;
+    d.v[i - 1] = (int64_t)cd & LB_S62_M;
+    cd >>= 62;
+    e.v[i - 1] = (int64_t)ce & LB_S62_M;
+    ce >>= 62;
+  }
+  d.v[6] = (int64_t)cd;
+  e.v[6] = (int64_t)ce;
+}
+// r in (-2p, p) -> r * sign (sign = +-1 as the sign of the top limb of f) in [0, p)
+LB_HD void lb_s62_normalize(lb_s62& r, int64_t sign) {
+  const lb_s62 M = lb_s62_p();
+  int64_t cond = r.v[6] >> 63;
+  LB_UNROLL for (int i = 0; i < 7; i++) r.v[i] += M.v[i] & cond;
+  const int64_t neg = sign >> 63;
+  LB_UNROLL for (int i = 0; i < 7; i++) r.v[i] = (r.v[i] ^ neg) - neg;
+  LB_UNROLL for (int i = 0; i < 6; i++) {
+    r.v[i + 1] += r.v[i] >> 62;
+    r.v[i] &= LB_S62_M;
+  }
+  cond = r.v[6] >> 63;
+  LB_UNROLL for (int i = 0; i < 7; i++) r.v[i] += M.v[i] & cond;
+  LB_UNROLL for (int i = 0; i < 6; i++) {
+    r.v[i + 1] += r.v[i] >> 62;
+    r.v[i] &= LB_S62_M;
+  }
+}
+LB_HD uint64_t lb_bits64(const uint32_t* w, int off, int nbits) {  // bits [off, off + nbits) of 12 words
+  const int q = off >> 5, s = off & 31;
+  uint64_t x = 0;
+  LB_UNROLL for (int k = 0; k < 3; k++) {
+    const int j = q + k;
+    const uint64_t wj = j < 12 ? w[j] : 0u;
+    if (k == 0) x = wj >> s;
+    else x |= (32 * k - s) < 64 ? wj << (32 * k - s) : 0;
+  }
+  return nbits >= 64 ? x : (x & ((1ULL << nbits) - 1));
+}
+// plain a in [0, p) -> a^-1 mod p (plain), 0 -> 0
+LB_HD fp fp_inv_plain_by_i(const fp& a) {
+  if (fp_is_zero(a)) return a;
+  lb_s62 f = lb_s62_p(), g, d, e;
+  LB_UNROLL for (int i = 0; i < 7; i++) {
+    g.v[i] = (int64_t)lb_bits64(a.v, 62 * i, 62);
+    d.v[i] = 0;
+    e.v[i] = i == 0;
+  }
+  int64_t eta = -1, t[4];
+  for (int it = 0; it < 40; it++) {  // (a 381-bit modulus needs <= 18 jumps)
+    eta = lb_divsteps62(eta, (uint64_t)f.v[0], (uint64_t)g.v[0], t);
+    lb_s62_update_de(d, e, t);
+    lb_s62_update_fg(f, g, t);
+    if (g.v[0] == 0) {
+      int64_t any = 0;
+      LB_UNROLL for (int i = 1; i < 7; i++) any |= g.v[i];
+      if (any == 0) break;
+    }
+  }
+  lb_s62_normalize(d, f.v[6]);  // f = +-1: the sign of its top limb
+  fp r;
+  LB_UNROLL for (int w = 0; w < 12; w++) {
+    const int b = 32 * w, i = b / 62, sft = b - 62 * i;
+    uint64_t x = (uint64_t)d.v[i] >> sft;
+    if (i + 1 < 7 && sft > 30) x |= (uint64_t)d.v[i + 1] << (62 - sft);
+    r.v[w] = (uint32_t)x;
+  }
+  return r;
+}
+#ifndef LB_INV_EEA
+#define LB_INV_EEA 0  // 1: the binary extended Euclid above (A/B)
+#endif
+LB_NI fp fp_inv_plain_vt(fp a) { return LB_INV_EEA ? fp_inv_plain_vt_i(a) : fp_inv_plain_by_i(a); }
 // Montgomery a R -> a^-1 R:  plain inverse of (a R) is a^-1 R^-1; times R^3 / R gives a^-1 R
 LB_HD fp fp_inv(const fp& a) { return fp_mul(fp_inv_plain_vt(a), fp_load(LB_R3)); }  // inv(0)=0
-LB_HD fp fp_inv_i(const fp& a) { return fp_mul(fp_inv_plain_vt_i(a), fp_load(LB_R3)); }
+LB_HD fp fp_inv_i(const fp& a) {
+  return fp_mul(LB_INV_EEA ? fp_inv_plain_vt_i(a) : fp_inv_plain_by_i(a), fp_load(LB_R3));
+}
 #ifndef LB_POW_INL
 #define LB_POW_INL true  // exponentiations with inline products (A/B: false = out-of-line fp_mul_v)
 #endif

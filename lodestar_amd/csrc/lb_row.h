@@ -180,40 +180,46 @@ struct r_cx_const {
   __device__ __forceinline__ int operator[](int i) const { return a[i]; }
 };
 
-// limb-sum reduction: v (64-bit limb sums) -> v - q p with q = floor(v / p) from the top limbs
-__device__ __forceinline__ int r_reduce(int64_t acc, int k) {
+// limb-sum reduction: v (64-bit limb sums) -> v - q p with q = floor(v / p) from the top limbs;
+// pk = p's limb for this lane (r_plimb, hoisted by the callers)
+__device__ __forceinline__ int r_reduce(int64_t acc, int k, int pk) {
   const int64_t a12 = r_dpp64<LBR_SHR(1)>(acc);  // lane 13 sees limb 12
   const double w = (double)acc * 268435456.0 + (double)a12;
   int q = (int)floor(w * LBR_INV_P336);
   q = r_bcast13(q);
-  acc -= (int64_t)q * r_plimb(k);
+  acc -= (int64_t)q * pk;
   return r_norm<true>(acc, k);
 }
+__device__ __forceinline__ int r_reduce(int64_t acc, int k) { return r_reduce(acc, k, r_plimb(k)); }
 
 // operand / linear sum over `n` (<= 8 * NB) (slot, coef) pairs at LDS words rec[0..n): the pair
 // words of a block of 8 and then their 8 limbs are loaded together (one LDS round trip each per
 // block instead of two per term)
+// Branch-free: every term of a block reads a valid record word (index clamped to n - 1; n >= 1)
+// and its slot, the terms past n get coefficient 0, so the block's 8 record reads and then its 8
+// limb reads issue together (guarded loads compiled to a branch per term).
 template <int NB>
 __device__ __forceinline__ int64_t r_acc(const lds_i32* S, const lds_i32* rec, int n, int k) {
   int64_t acc = 0;
   LB_UNROLL for (int b = 0; b < NB; b++) {
     if (8 * b < n) {
       int w[8], v[8];
-      LB_UNROLL for (int j = 0; j < 8; j++) w[j] = 8 * b + j < n ? rec[8 * b + j] : 0;
-      LB_UNROLL for (int j = 0; j < 8; j++) v[j] = 8 * b + j < n ? S[16 * (w[j] & 0xffff) + k] : 0;
-      LB_UNROLL for (int j = 0; j < 8; j++) acc += (int64_t)(w[j] >> 16) * v[j];
+      LB_UNROLL for (int j = 0; j < 8; j++) w[j] = rec[min(8 * b + j, n - 1)];
+      LB_UNROLL for (int j = 0; j < 8; j++) v[j] = S[16 * (w[j] & 0xffff) + k];
+      LB_UNROLL for (int j = 0; j < 8; j++) acc += (int64_t)(8 * b + j < n ? (w[j] >> 16) : 0) * v[j];
     }
   }
   return acc;
 }
 template <int NB>
-__device__ __forceinline__ int r_sum(const lds_i32* S, const lds_i32* rec, int n, int k) {
-  return r_reduce(r_acc<NB>(S, rec, n, k), k);
+__device__ __forceinline__ int r_sum(const lds_i32* S, const lds_i32* rec, int n, int k, int pk) {
+  return r_reduce(r_acc<NB>(S, rec, n, k), k, pk);
 }
 // a product operand: with a coefficient sum <= 16 (phase flag clear) only the limb carries run
-__device__ __forceinline__ int r_operand(const lds_i32* S, const lds_i32* rec, int n, int k, bool red) {
+__device__ __forceinline__ int r_operand(const lds_i32* S, const lds_i32* rec, int n, int k, bool red, int pk) {
   const int64_t acc = r_acc<1>(S, rec, n, k);
-  return red ? r_reduce(acc, k) : r_norm<true>(acc, k);
+  if (red) return r_reduce(acc, k, pk);
+  return r_norm<true>(acc, k);
 }
 
 __device__ __forceinline__ void r_load_rep(const lds_i32* S, int slot, int (&x)[14]) {
@@ -236,7 +242,7 @@ __device__ __forceinline__ const lds_i32* r_progs(int32_t* S) {
 __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
   lds_i32* S = r_lds(S_generic);
   const lds_i32* prog = r_progs(S_generic) + off;
-  const int k = r_limb(), row = r_row();
+  const int k = r_limb(), row = r_row(), pk = r_plimb(k);
   const int nph = __builtin_amdgcn_readfirstlane(prog[0]), nout = __builtin_amdgcn_readfirstlane(prog[1]);
   int pos = 2 + nout;
   for (int ph = 0; ph < nph; ph++) {
@@ -251,13 +257,13 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
         if (t < n) {
           const lds_i32* rec = prog + pos + t * rs;
           const int dst = rec[0];
-          const int y = (flags & 2) ? S[16 * (rec[1 + nx] & 0xffff) + k] : r_operand(S, rec + 1 + nx, ny, k, flags & 8);
+          const int y = (flags & 2) ? S[16 * (rec[1 + nx] & 0xffff) + k] : r_operand(S, rec + 1 + nx, ny, k, flags & 8, pk);
           int xs;
           if (flags & 1) {
             xs = rec[1] & 0xffff;
           } else {
             xs = LBR_ROWX + row;
-            S[16 * xs + k] = r_operand(S, rec + 1, nx, k, flags & 4);
+            S[16 * xs + k] = r_operand(S, rec + 1, nx, k, flags & 4, pk);
           }
           int x[14];
           r_load_rep(S, xs, x);
@@ -271,7 +277,7 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
         const int t = base + row;
         if (t < n) {
           const lds_i32* rec = prog + pos + t * rs;
-          S[16 * rec[0] + k] = r_sum<3>(S, rec + 1, nx, k);
+          S[16 * rec[0] + k] = r_sum<3>(S, rec + 1, nx, k, pk);
         }
       }
       pos += n * rs;

@@ -48,6 +48,8 @@ __global__ void __launch_bounds__(LBR_NT) k_row_ops(int iters, uint64_t* out) {
     if (OP == 3) r_exec(S, LBR_SQR12);
     if (OP == 4) r_csqr(S, LBR_A(0), LBR_A(0));
     if (OP == 5) r_final_exp(S, LBR_A(0), LBR_A(0));
+    if (OP == 6) r_inv(S, LBR_A(2), LBR_A(0), LBR_A(3), LBR_A(4), LBR_A(5));
+    if (OP == 7) r_pow_xabs(S, LBR_A(2), LBR_A(0));
   }
   r_sync();
   const uint64_t t1 = rt();
@@ -161,11 +163,24 @@ __global__ void k_cmp(const int* xin, const int* yin, int* o16, int* o32) {
   }
 }
 
+template <int T>
+__global__ void __launch_bounds__(T) k_inv_chain(int iters, uint64_t* out, uint32_t* sink) {
+  fp a = fp_one();
+  a.v[0] ^= threadIdx.x + 12345;
+  a.v[5] ^= 0x9e3779b9u;
+  const uint64_t t0 = rt();
+  if (threadIdx.x == 0)
+    for (int it = 0; it < iters; it++) a = fp_inv_i(fp_add(a, fp_one()));
+  __syncthreads();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = a.v[0];
+}
 int main() {
   uint64_t* d;
   int* sink;
   hipMalloc(&d, 64);
-  hipMalloc(&sink, 4096);
+  hipMalloc(&sink, 8192);
   uint64_t h;
   auto run = [&](const char* name, auto launch, int iters) {
     launch(iters);  // warm
@@ -194,6 +209,10 @@ int main() {
   run("row copy12", [&](int n) { hipLaunchKernelGGL(k_row_ops<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row exec SQR12 only", [&](int n) { hipLaunchKernelGGL(k_row_ops<3>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row CSQR12", [&](int n) { hipLaunchKernelGGL(k_row_ops<4>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("fp_inv_i lane0 (64 thr)", [&](int n) { hipLaunchKernelGGL(k_inv_chain<64>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 50);
+  run("fp_inv_i lane0 (1024 thr)", [&](int n) { hipLaunchKernelGGL(k_inv_chain<1024>, dim3(1), dim3(1024), 0, 0, n, d, (uint32_t*)sink); }, 50);
+  run("row inv", [&](int n) { hipLaunchKernelGGL(k_row_ops<6>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 20);
+  run("row pow_xabs", [&](int n) { hipLaunchKernelGGL(k_row_ops<7>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 5);
   run("row final exp", [&](int n) { hipLaunchKernelGGL(k_row_ops<5>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 3);
   {
     unsigned long long* dd;
