@@ -168,6 +168,9 @@ struct lb_engine {
   uint32_t miller_lds3_max = 32768;
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
+  // ... and with a workgroup per root on the row engine while the device is alone.  LB_HASH_ROW_MAX.
+  uint32_t hash_row_max = 16;
+  uint32_t hash_row_careful = 0;  // LB_HASH_ROW_CAREFUL=1: the exceptional-case path always (tests)
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
   uint32_t subgroup_g8_max = 4096;
   // ... and S = sum r_i sig_i by per-set 8-lane scalar multiplications + trees instead of the
@@ -300,6 +303,10 @@ static inline uint32_t nblk_inv(uint32_t n) { return (n + LB_INV_TPB - 1) / LB_I
 
 static int fill_scalars(lb_engine* e, uint32_t n, const uint64_t* user) {
   e->h_scalars.resize(n);
+  if (!user && n == 1) {
+    e->h_scalars[0] = 1;  // one set: verified unblinded (k_sig_unblinded), as Signature.verify
+    return LB_OK;
+  }
   if (user) {
     for (uint32_t i = 0; i < n; i++)
       if (user[i] == 0) return LB_BAD_SCALAR;
@@ -385,6 +392,8 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* ml = getenv("LB_MILLER_LDS3_MAX")) e->miller_lds3_max = (uint32_t)strtoul(ml, nullptr, 10);
   if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
+  if (const char* hr = getenv("LB_HASH_ROW_MAX")) e->hash_row_max = (uint32_t)strtoul(hr, nullptr, 10);
+  if (const char* hc = getenv("LB_HASH_ROW_CAREFUL")) e->hash_row_careful = (uint32_t)strtoul(hc, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
   if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
@@ -962,7 +971,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       // 8 lanes per root when the device runs no other batch (a few hundred waves on 1 024 SIMDs:
       // latency), one lane per root under load (2.5x less work), as for the Miller loops below
       const bool alone = e->miller_form == 0 && device_alone(e);
-      if (nuh <= e->hash_g8_max || (LB_HASH_ALONE_G8 && alone))
+      if (nuh <= e->hash_row_max && e->alone && e->row_fe)
+        hipLaunchKernelGGL(k_hash_finish_row, dim3(nuh), dim3(LBR_NT), 0, s1, n, nu, e->q.as<uint32_t>(),
+                           e->h_aff.as<uint32_t>(), e->hash_row_careful);
+      else if (nuh <= e->hash_g8_max || (LB_HASH_ALONE_G8 && alone))
         hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
                            e->h_aff.as<uint32_t>());
       else
@@ -974,7 +986,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       }
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
-    if (n <= e->small_s_max) {
+    if (n == 1 && !scalars) {
+      stage_scope sc(e, ST_SIG_MSM, s2);
+      hipLaunchKernelGGL(k_sig_unblinded, dim3(1), dim3(64), 0, s2, e->sig_aff.as<uint32_t>(),
+                         e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), 2 * mj, e->treeS.as<uint32_t>());
+    } else if (n <= e->small_s_max) {
       stage_scope sc(e, ST_SIG_MSM, s2);
       LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
       LB_HIP(e->s_part.ensure((size_t)((n + 63) / 64) * sizeof(g2j)));

@@ -77,7 +77,25 @@ __device__ __forceinline__ int64_t r_dpp64(int64_t v) {
 #define LBR_SHR(n) (0x110 + (n))  // lane k <- lane k - n of the row (0 below the row)
 #define LBR_SHL(n) (0x100 + (n))  // lane k <- lane k + n of the row (0 above the row)
 // broadcast lane 13 of each row (ds_swizzle bit mode: lane' = (lane & 0x10) | 13 within 32)
-__device__ __forceinline__ int r_bcast13(int v) { return __builtin_amdgcn_ds_swizzle(v, 0x10 | (13 << 5)); }
+// lane I of the row to every lane of the row (DPP row_newbcast: a VALU move, no LDS round trip)
+template <int I>
+__device__ __forceinline__ int r_bcast(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + I, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int r_bcast13(int v) {
+#ifdef LBR_SWIZZLE_BCAST
+  return __builtin_amdgcn_ds_swizzle(v, 0x10 | (13 << 5));
+#else
+  return r_bcast<13>(v);
+#endif
+}
+// a distributed element (lane k: limb k) replicated in every lane of the row
+__device__ __forceinline__ void r_rep(int v, int (&x)[14]) {
+  x[0] = r_bcast<0>(v); x[1] = r_bcast<1>(v); x[2] = r_bcast<2>(v); x[3] = r_bcast<3>(v);
+  x[4] = r_bcast<4>(v); x[5] = r_bcast<5>(v); x[6] = r_bcast<6>(v); x[7] = r_bcast<7>(v);
+  x[8] = r_bcast<8>(v); x[9] = r_bcast<9>(v); x[10] = r_bcast<10>(v); x[11] = r_bcast<11>(v);
+  x[12] = r_bcast<12>(v); x[13] = r_bcast<13>(v);
+}
 
 #define LBR_M28 0x0fffffff
 struct lbr_k {
@@ -237,8 +255,153 @@ __device__ __forceinline__ const lds_i32* r_progs(int32_t* S) {
   return s + LBR_SLOT_WORDS + LBR_MISC - s[LBR_SLOT_WORDS + 0];
 }
 
+// ---------------------------------------------------------------- the interpreter
+// Software-pipelined: the program words a row needs for phase ph + 1 (the header, and its task
+// record: destination and up to 16 (slot, coef) pairs) are read while phase ph's product runs
+// (program words are read-only, so only the slot reads wait for the barrier); one LDS round trip
+// (the slot limbs) remains between a barrier and the product instead of four (header, record,
+// slots; the operand's replicated copy).  Tasks past the first LBR_NROWS of a phase take the
+// unpipelined path (r_exec_tail).
+struct r_pref {
+  int dst;
+  int w[16];
+};
+__device__ __forceinline__ void r_prefetch(const lds_i32* prog, int pos, int h0, int h1, int row, r_pref& p) {
+  const int kind = h0 & 0xff, n = h0 >> 16, nx = h1 & 0xffff, ny = h1 >> 16;
+  int t, rs, nA, offB, nB;
+  if (kind == 0) {
+    t = row;
+    rs = 1 + nx + ny;
+    nA = nx;
+    offB = 1 + nx;
+    nB = ny;
+  } else {
+    t = (row - ny + 4 * LBR_NROWS) % LBR_NROWS;
+    rs = 1 + nx;
+    nA = min(nx, 8);
+    offB = 9;
+    nB = nx - 8;
+  }
+  t = min(t, n - 1);  // idle rows read a valid record (unused)
+  const lds_i32* rec = prog + pos + t * rs;
+  p.dst = rec[0];
+  LB_UNROLL for (int j = 0; j < 8; j++) p.w[j] = rec[1 + min(j, nA - 1)];
+  LB_UNROLL for (int j = 0; j < 8; j++) p.w[8 + j] = rec[nB > 0 ? offB + min(j, nB - 1) : 1];
+}
+// sum of up to 8 prefetched terms w[O .. O + 8) (n of them; the rest coefficient 0)
+template <int O>
+__device__ __forceinline__ int64_t r_acc_w(const lds_i32* S, const r_pref& p, int n, int k) {
+  int v[8];
+  LB_UNROLL for (int j = 0; j < 8; j++) v[j] = S[16 * (p.w[O + j] & 0xffff) + k];
+  int64_t acc = 0;
+  LB_UNROLL for (int j = 0; j < 8; j++) acc += (int64_t)(j < n ? (p.w[O + j] >> 16) : 0) * v[j];
+  return acc;
+}
+template <int O>
+__device__ __forceinline__ int r_operand_w(const lds_i32* S, const r_pref& p, int n, bool plain, bool red, int k,
+                                           int pk) {
+  if (plain) return S[16 * (p.w[O] & 0xffff) + k];
+  const int64_t acc = r_acc_w<O>(S, p, n, k);
+  return red ? r_reduce(acc, k, pk) : r_norm<true>(acc, k);
+}
+// tasks LBR_NROWS.. of a phase (records at prog + pos)
+__device__ void r_exec_tail(lds_i32* S, const lds_i32* prog, int pos, int h0, int h1) {
+  const int k = r_limb(), row = r_row(), pk = r_plimb(k);
+  const int kind = h0 & 0xff, flags = (h0 >> 8) & 0xff, n = h0 >> 16;
+  const int nx = h1 & 0xffff, ny = h1 >> 16;
+  if (kind == 0) {
+    const int rs = 1 + nx + ny;
+    for (int base = LBR_NROWS; base < n; base += LBR_NROWS) {
+      const int t = base + row;
+      if (t < n) {
+        const lds_i32* rec = prog + pos + t * rs;
+        const int y = (flags & 2) ? S[16 * (rec[1 + nx] & 0xffff) + k] : r_operand(S, rec + 1 + nx, ny, k, flags & 8, pk);
+        int x[14];
+        r_rep((flags & 1) ? S[16 * (rec[1] & 0xffff) + k] : r_operand(S, rec + 1, nx, k, flags & 4, pk), x);
+        S[16 * rec[0] + k] = rp_mul(x, y, k);
+      }
+    }
+  } else {
+    const int rs = 1 + nx, rr = (row - ny + 4 * LBR_NROWS) % LBR_NROWS;
+    for (int base = LBR_NROWS; base < n; base += LBR_NROWS) {
+      const int t = base + rr;
+      if (t < n) {
+        const lds_i32* rec = prog + pos + t * rs;
+        S[16 * rec[0] + k] = r_sum<3>(S, rec + 1, nx, k, pk);
+      }
+    }
+  }
+}
+
+#ifndef LBR_EXEC_V1
 // Run one program (offset `off` in the image): inputs already in IN, outputs left in the temps
 // the header lists.
+__device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
+  lds_i32* S = r_lds(S_generic);
+  const lds_i32* prog = r_progs(S_generic) + off;
+  const int k = r_limb(), row = r_row(), pk = r_plimb(k);
+  const int nph = __builtin_amdgcn_readfirstlane(prog[0]), nout = __builtin_amdgcn_readfirstlane(prog[1]);
+  int pos = 2 + nout;
+  int h0 = __builtin_amdgcn_readfirstlane(prog[pos]), h1 = __builtin_amdgcn_readfirstlane(prog[pos + 1]);
+  pos += 2;
+  r_pref p;
+  r_prefetch(prog, pos, h0, h1, row, p);
+  for (int ph = 0; ph < nph; ph++) {
+    const int kind = h0 & 0xff, flags = (h0 >> 8) & 0xff, n = h0 >> 16;
+    const int nx = h1 & 0xffff, ny = h1 >> 16;
+    const int npos = pos + n * (kind == 0 ? 1 + nx + ny : 1 + nx);
+    const bool more = ph + 1 < nph;
+    int nh0v = 0, nh1v = 0;
+    if (more) {
+      nh0v = prog[npos];
+      nh1v = prog[npos + 1];
+    }
+    const int dst = p.dst;
+    int yv = 0, xv = 0;
+    bool act;
+    if (kind == 0) {
+      act = row < n;
+      if (act) {
+        yv = r_operand_w<8>(S, p, ny, flags & 2, flags & 8, k, pk);
+        xv = r_operand_w<0>(S, p, nx, flags & 1, flags & 4, k, pk);
+      }
+    } else {
+      act = (row - ny + 4 * LBR_NROWS) % LBR_NROWS < n;
+      if (act) {
+        int64_t acc = r_acc_w<0>(S, p, min(nx, 8), k);
+        if (nx > 8) acc += r_acc_w<8>(S, p, nx - 8, k);
+        if (nx > 16) {
+          const int t = (row - ny + 4 * LBR_NROWS) % LBR_NROWS;
+          acc += r_acc<1>(S, prog + pos + t * (1 + nx) + 17, nx - 16, k);
+        }
+        yv = r_reduce(acc, k, pk);
+      }
+    }
+    int nh0 = 0, nh1 = 0;
+    if (more) {
+      nh0 = __builtin_amdgcn_readfirstlane(nh0v);
+      nh1 = __builtin_amdgcn_readfirstlane(nh1v);
+      r_prefetch(prog, npos + 2, nh0, nh1, row, p);
+    }
+    if (act) {
+      if (kind == 0) {
+        int x[14];
+        r_rep(xv, x);
+        yv = rp_mul(x, yv, k);
+      }
+      S[16 * dst + k] = yv;
+    }
+    if (n > LBR_NROWS) r_exec_tail(S, prog, pos, h0, h1);
+    if (kind != 0 || !(flags & 16)) r_sync();  // flag 16: the next (linear) phase reads nothing of this one
+#ifdef LBR_PHASE_HOOK
+    LBR_PHASE_HOOK(ph, kind, n);
+#endif
+    pos = npos + 2;
+    h0 = nh0;
+    h1 = nh1;
+  }
+}
+#else
 __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
   lds_i32* S = r_lds(S_generic);
   const lds_i32* prog = r_progs(S_generic) + off;
@@ -257,7 +420,15 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
         if (t < n) {
           const lds_i32* rec = prog + pos + t * rs;
           const int dst = rec[0];
+#ifdef LBR_SUB_HOOK
+          LBR_SUB_HOOK(1, dst);
+#endif
           const int y = (flags & 2) ? S[16 * (rec[1 + nx] & 0xffff) + k] : r_operand(S, rec + 1 + nx, ny, k, flags & 8, pk);
+#ifdef LBR_SUB_HOOK
+          LBR_SUB_HOOK(2, y);
+#endif
+          int x[14];
+#ifdef LBR_LDS_REP
           int xs;
           if (flags & 1) {
             xs = rec[1] & 0xffff;
@@ -265,16 +436,27 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
             xs = LBR_ROWX + row;
             S[16 * xs + k] = r_operand(S, rec + 1, nx, k, flags & 4, pk);
           }
-          int x[14];
           r_load_rep(S, xs, x);
-          S[16 * dst + k] = rp_mul(x, y, k);
+#else
+          r_rep((flags & 1) ? S[16 * (rec[1] & 0xffff) + k] : r_operand(S, rec + 1, nx, k, flags & 4, pk), x);
+#endif
+#ifdef LBR_SUB_HOOK
+          LBR_SUB_HOOK(3, x[13]);
+#endif
+          const int rv = rp_mul(x, y, k);
+#ifdef LBR_SUB_HOOK
+          LBR_SUB_HOOK(4, rv);
+#endif
+          S[16 * dst + k] = rv;
         }
       }
       pos += n * rs;
     } else {
-      const int rs = 1 + nx;
+      // ny: row offset (a linear phase merged into the product phase before it runs on the rows
+      // after the products')
+      const int rs = 1 + nx, rr = (row - ny + 4 * LBR_NROWS) % LBR_NROWS;
       for (int base = 0; base < n; base += LBR_NROWS) {
-        const int t = base + row;
+        const int t = base + rr;
         if (t < n) {
           const lds_i32* rec = prog + pos + t * rs;
           S[16 * rec[0] + k] = r_sum<3>(S, rec + 1, nx, k, pk);
@@ -282,12 +464,13 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
       }
       pos += n * rs;
     }
-    r_sync();
+    if (kind != 0 || !(flags & 16)) r_sync();  // flag 16: the next (linear) phase reads nothing of this one
 #ifdef LBR_PHASE_HOOK
     LBR_PHASE_HOOK(ph, kind, n);
 #endif
   }
 }
+#endif  // LBR_EXEC_V1
 
 // ---------------------------------------------------------------- element moves (limb-parallel)
 // dst[e] = src(e) for e < n (src(e) a slot index; every source read before any write)
@@ -306,6 +489,14 @@ __device__ __forceinline__ void r_gather(int32_t* S_generic, int dst, int n, F s
     const int e = row + LBR_NROWS * j;
     if (e < n) S[16 * (dst + e) + k] = v[j];
   }
+  r_sync();
+}
+// the same when source and destination slots are disjoint (one barrier)
+template <class F>
+__device__ __forceinline__ void r_gather_dj(int32_t* S_generic, int dst, int n, F src) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row();
+  for (int e = row; e < n; e += LBR_NROWS) S[16 * (dst + e) + k] = S[16 * src(e) + k];
   r_sync();
 }
 __device__ __forceinline__ void r_copy(int32_t* S, int dst, int src, int n) {
@@ -608,4 +799,135 @@ __device__ void r_miller(int32_t* S_generic, int dst) {
     }
   }
   r_conj(S_generic, dst, dst);
+}
+
+// ---------------------------------------------------------------- G2 points (6 slots: X, Y, Z in Fp2)
+// hash_to_G2's cofactor clearing on rows (k_hash_finish_row): the chain of lb_group.h
+// g8_clear_cofactor_st with every doubling / addition one row program (G2DBL: 16 products in 3
+// levels, G2ADD: 43 products; tools/gen_row_programs.py g2_dbl / g2_add).  Infinity is a zero Z
+// (a doubling keeps it); each addition tests its operands' Z and its H and r (canonical values,
+// one lane per slot) for the exceptional cases, as jac_add_i / g8_add do.
+// bit e of the result: slot src(e) is 0 mod p (e < n <= 16)
+template <class F>
+__device__ uint32_t r_zero_mask(int32_t* S_generic, int n, F src) {
+  lds_i32* S = r_lds(S_generic);
+  const int t = r_tid();
+  if (t == 0) S[LBR_SLOT_WORDS + 2] = 0;
+  r_sync();
+  if (t < n) {
+    int32_t l[14];
+    const int s = src(t);
+    LB_UNROLL for (int k = 0; k < 14; k++) l[k] = S[16 * s + k];
+    if (fp_is_zero(r_canon(l))) atomicOr((int*)&S_generic[LBR_SLOT_WORDS + 2], 1 << t);
+  }
+  r_sync();
+  const uint32_t m = (uint32_t)S[LBR_SLOT_WORDS + 2];
+  r_sync();
+  return m;
+}
+// program outputs (temps) to disjoint slots
+__device__ __forceinline__ void r_out_dj(int32_t* S, int off, int first, int n, int dst) {
+  const lds_i32* prog = r_progs(S) + off;
+  r_gather_dj(S, dst, n, [&](int e) { return prog[2 + first + e]; });
+}
+__device__ void r_g2_dbl(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 6);
+  r_exec(S, LBR_G2DBL);
+  r_out(S, LBR_G2DBL, 0, 6, dst);
+}
+__device__ void r_g2_psi(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 6);
+  r_exec(S, LBR_PSI);
+  r_out(S, LBR_PSI, 0, 6, dst);
+}
+__device__ void r_g2_psi2(int32_t* S, int dst, int a) {
+  r_copy(S, LBR_IN, a, 6);
+  r_exec(S, LBR_PSI2);
+  r_out(S, LBR_PSI2, 0, 6, dst);
+}
+// a = -a (Y negated limb-wise, as r_conj)
+__device__ void r_g2_neg(int32_t* S_generic, int a) {
+  lds_i32* S = r_lds(S_generic);
+  const int t = r_tid();
+  if (t < 32) S[16 * (a + 2) + t] = -S[16 * (a + 2) + t];
+  r_sync();
+}
+// dst = a + b (dst may alias a or b)
+__device__ void r_g2_add(int32_t* S_generic, int dst, int a, int b) {
+  r_gather(S_generic, LBR_IN, 12, [&](int e) { return e < 6 ? a + e : b + e - 6; });
+  r_exec(S_generic, LBR_G2ADD);
+  const lds_i32* prog = r_progs(S_generic) + LBR_G2ADD;
+  // bits 0-1: a's Z, 2-3: b's Z, 4-5: H, 6-7: r (G2ADD's outputs 6..9)
+  const uint32_t m = r_zero_mask(S_generic, 8, [&](int e) { return e < 2 ? a + 4 + e : (e < 4 ? b + 2 + e : prog[4 + e]); });
+  if ((m & 0xc) == 0xc) {  // b = O
+    if (dst != a) r_copy(S_generic, dst, a, 6);
+  } else if ((m & 0x3) == 0x3) {  // a = O
+    if (dst != b) r_copy(S_generic, dst, b, 6);
+  } else if ((m & 0x30) == 0x30) {  // a = +-b
+    if ((m & 0xc0) == 0xc0) r_g2_dbl(S_generic, dst, a);
+    else r_gather(S_generic, dst, 6, [&](int) { return LBR_CONST + LBR_C_ZERO; });
+  } else {
+    r_out(S_generic, LBR_G2ADD, 0, 6, dst);
+  }
+}
+// dst = [|x|] a (dst must not alias a).  FAST: the accumulator stays in IN (slots 0..5, the base
+// in 6..11), each step one program and one move of its outputs back into IN; additions without
+// the exceptional-case tests (see r_g2_clear_cofactor).
+template <bool FAST>
+__device__ void r_g2_mul_xabs(int32_t* S, int dst, int a) {
+  if (FAST) {
+    r_gather_dj(S, LBR_IN, 12, [&](int e) { return a + (e < 6 ? e : e - 6); });
+    for (int i = 62; i >= 0; i--) {
+      r_exec(S, LBR_G2DBL);
+      r_out_dj(S, LBR_G2DBL, 0, 6, LBR_IN);
+      if ((LB_X_ABS >> i) & 1ull) {
+        r_exec(S, LBR_G2ADD);
+        r_out_dj(S, LBR_G2ADD, 0, 6, LBR_IN);
+      }
+    }
+    r_gather_dj(S, dst, 6, [&](int e) { return LBR_IN + e; });
+    return;
+  }
+  r_copy(S, dst, a, 6);
+  for (int i = 62; i >= 0; i--) {
+    r_g2_dbl(S, dst, dst);
+    if ((LB_X_ABS >> i) & 1ull) r_g2_add(S, dst, dst, a);
+  }
+}
+// dst = a + b without the exceptional cases (dst may alias a or b)
+__device__ void r_g2_add_fast(int32_t* S, int dst, int a, int b) {
+  r_gather_dj(S, LBR_IN, 12, [&](int e) { return e < 6 ? a + e : b + e - 6; });
+  r_exec(S, LBR_G2ADD);
+  r_out_dj(S, LBR_G2ADD, 0, 6, dst);
+}
+// h_eff p via psi (as g8_clear_cofactor_st) for p in slots p .. p + 5; result in dst.  Uses
+// areas 0..2 besides.  FAST: no exceptional-case tests.  Every exceptional case of the
+// formulas (an operand at infinity, P = +-Q in an addition, a doubling of a point of order 2)
+// yields Z = 0, and a zero Z stays zero through every later doubling, addition, psi and psi^2:
+// a FAST result with Z != 0 is exact; Z = 0 (negligible probability for hash outputs) is
+// recomputed with the tests (k_hash_finish_row).
+template <bool FAST>
+__device__ void r_g2_clear_cofactor(int32_t* S, int dst, int p) {
+  const int T1 = LBR_A(0), T3 = LBR_A(0) + 6, T2 = LBR_A(1), X = LBR_A(1) + 6, W = LBR_A(2);
+  auto add = [&](int d, int a, int b) {
+    if (FAST) r_g2_add_fast(S, d, a, b);
+    else r_g2_add(S, d, a, b);
+  };
+  r_g2_mul_xabs<FAST>(S, T1, p);
+  r_g2_neg(S, T1);  // t1 = [x] p
+  r_g2_dbl(S, T3, p);
+  r_g2_psi2(S, T3, T3);
+  r_g2_psi(S, T2, p);
+  r_copy(S, W, T2, 6);
+  r_g2_neg(S, W);
+  add(T3, T3, W);  // psi^2(2p) - psi(p)
+  add(T2, T2, T1);  // psi(p) + t1
+  r_g2_mul_xabs<FAST>(S, X, T2);
+  r_g2_neg(S, X);  // [x](t1 + t2)
+  add(T3, T3, X);
+  r_g2_neg(S, T1);
+  add(T3, T3, T1);
+  r_copy(S, W, p, 6);
+  r_g2_neg(S, W);
+  add(dst, T3, W);
 }

@@ -732,3 +732,43 @@ def test_speculative_per_root_chain(monkeypatch, spec):
                 assert np.array_equal(b.search_after_partial(), wl.expected), name
             finally:
                 b.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_row_engine_forms_agree(monkeypatch, name):
+    """The row engine's forms (lb_row.h: a workgroup per root / per product-tree node, every Fp
+    product on a 16-lane row) run only while the device is alone: hash_to_G2's cofactor clearing
+    (k_hash_finish_row, its fast path and, LB_HASH_ROW_CAREFUL=1, the path with the exceptional-
+    case tests), the Miller loops and tree nodes (LB_ROW_MAX), ML(-G1, S), the root checks and
+    partials (LB_ROW_FE).  Against the wave / 8-lane forms (all row forms off) on the same batch
+    and blinding scalars: same verdicts, byte-identical root partials (576-byte Fp12 products
+    before the final exponentiation).  c1 (one set) takes the unblinded path (scalar 1)."""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    outs = []
+    big = str(1 << 20)
+    for row_fe, row_max, hash_max, careful in (("1", None, None, "0"), ("0", "0", "0", "0"),
+                                               ("1", "64", big, "1")):
+        monkeypatch.setenv("LB_ROW_FE", row_fe)
+        monkeypatch.setenv("LB_HASH_ROW_CAREFUL", careful)
+        for var, val in (("LB_ROW_MAX", row_max), ("LB_HASH_ROW_MAX", hash_max)):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, val)
+        with Engine(0) as e:
+            wl = W.make(e, name)
+            b = e.upload(W.indexed_for(e, wl))
+            try:
+                sc = None
+                if wl.packed.n_sets > 1:
+                    sc = np.random.default_rng(7).integers(1, 1 << 63, size=wl.packed.n_sets, dtype=np.uint64)
+                got = np.asarray(b.verify(scalars=sc))[:wl.packed.n_jobs]
+                part = bytes(b.partial(scalars=sc)[0])
+            finally:
+                b.free()
+        assert (wl.expected == 1).all()
+        assert np.array_equal(got, wl.expected), (row_fe, row_max, np.nonzero(got != wl.expected))
+        outs.append(part)
+    assert outs[0] == outs[1] == outs[2]

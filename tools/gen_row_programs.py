@@ -159,6 +159,26 @@ class RowProg(G.Prog):
             return super().mul(self.mat(x), self.mat(y))
         return super().mul(x, y)
 
+    def mat(self, lin, force=False):
+        """Linear tasks of the same stage are inlined into the sum instead of read as slots (one
+        level, i.e. one phase and barrier, instead of a chain); tasks left unread are dropped by
+        encode.  (A/B: ROW_NO_FLATTEN=1.)"""
+        if os.environ.get("ROW_NO_FLATTEN") != "1":
+            lin = self._flatten(lin)
+        return super().mat(lin, force)
+
+    def _flatten(self, lin):
+        st = self._avail(lin)
+        defs = {l[2]: l[3] for l in self.lins if l[0] == st}
+        if not any(s in defs for s in lin.d):
+            return lin
+        out = G.Lin()
+        for s, c in lin.d.items():
+            out = out + (defs[s].scale(c) if s in defs else G.Lin({s: c}))
+        if len(out.d) > G.MAXL or sum(abs(c) for c in out.d.values()) > 64:
+            return lin
+        return out
+
 
 def f4sqr(t, a0, a1):
     """(a0 + a1 s)^2 in Fp4 = Fp2[s]/(s^2 - xi): (a0^2 + xi a1^2, (a0 + a1)^2 - a0^2 - a1^2)"""
@@ -188,9 +208,73 @@ def cyclotomic_sqr(t, a):
     return (r00, r01, r02), (r10, r11, r12)
 
 
+# extra constant slots of the row engine (after the wave programs' 19): psi's coefficients
+C_PSI_CX, C_PSI_CY, C_PSI2_CX, C_PSI2_CY = 19, 21, 23, 24
+N_CONST_ROW = 25
+
+
+def g2_in(pg, base):
+    return tuple((pg.inp(base + 2 * k), pg.inp(base + 2 * k + 1)) for k in range(3))
+
+
+def g2_dbl(t, P):
+    """2P, dbl-2009-l (as lb_curve.h jac_dbl_i / lb_group.h g8_dbl): 16 products in 3 levels"""
+    X, Y, Z = P
+    A = t.f2sqr(X)
+    B = t.f2sqr(Y)
+    YZ = t.f2mul(Y, Z)
+    C = t.f2sqr(B)
+    D = t.f2dbl(t.f2sub(t.f2sub(t.f2sqr(t.f2add(X, B)), A), C))
+    E = t.f2mul3(A)
+    F = t.f2sqr(E)
+    X3 = t.f2sub(F, t.f2dbl(D))
+    C8 = (C[0].scale(8), C[1].scale(8))
+    Y3 = t.f2sub(t.f2mul(E, t.f2sub(D, X3)), C8)
+    return X3, Y3, t.f2dbl(YZ)
+
+
+def g2_add(t, P, Q):
+    """P + Q, add-2007-bl (as jac_add_i without its exceptional cases; H and r are outputs so the
+    caller can detect them): 43 products"""
+    X1, Y1, Z1 = P
+    X2, Y2, Z2 = Q
+    Z1Z1 = t.f2sqr(Z1)
+    Z2Z2 = t.f2sqr(Z2)
+    U1 = t.f2mul(X1, Z2Z2)
+    U2 = t.f2mul(X2, Z1Z1)
+    S1 = t.f2mul(t.f2mul(Y1, Z2), Z2Z2)
+    S2 = t.f2mul(t.f2mul(Y2, Z1), Z1Z1)
+    H = t.f2sub(U2, U1)
+    I = t.f2sqr(t.f2dbl(H))
+    J = t.f2mul(H, I)
+    r = t.f2dbl(t.f2sub(S2, S1))
+    V = t.f2mul(U1, I)
+    X3 = t.f2sub(t.f2sub(t.f2sqr(r), J), t.f2dbl(V))
+    Y3 = t.f2sub(t.f2mul(r, t.f2sub(V, X3)), t.f2dbl(t.f2mul(S1, J)))
+    Z3 = t.f2mul(t.f2sub(t.f2sub(t.f2sqr(t.f2add(Z1, Z2)), Z1Z1), Z2Z2), H)
+    return (X3, Y3, Z3), H, r
+
+
+def g2_psi(t, pg, P):
+    X, Y, Z = P
+    cx = (pg.const(C_PSI_CX), pg.const(C_PSI_CX + 1))
+    cy = (pg.const(C_PSI_CY), pg.const(C_PSI_CY + 1))
+    return t.f2mul(t.f2conj(X), cx), t.f2mul(t.f2conj(Y), cy), t.f2conj(Z)
+
+
+def g2_psi2(t, pg, P):
+    X, Y, Z = P
+    return t.f2mulfp(X, pg.const(C_PSI2_CX)), t.f2mulfp(Y, pg.const(C_PSI2_CY)), Z
+
+
+def g2_flat(P):
+    return [c for x in P for c in x]
+
+
 def build_programs():
     """the wave programs' formulas (tools/gen_wave_programs.py build_programs) traced into
-    RowProg, plus CSQR12"""
+    RowProg, plus CSQR12 and the G2 point programs (G2DBL, G2ADD, PSI, PSI2) of the row engine's
+    cofactor clearing (lb_row.h r_g2_*)"""
     saved = G.Prog
     G.Prog = RowProg
     try:
@@ -199,6 +283,23 @@ def build_programs():
         t = G.T(pg)
         pg.output(G.fp12_flat(cyclotomic_sqr(t, G.fp12_in(pg, 0))))
         progs["CSQR12"] = pg
+        pg = RowProg("G2DBL")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_dbl(t, g2_in(pg, 0))))
+        progs["G2DBL"] = pg
+        pg = RowProg("G2ADD")
+        t = G.T(pg)
+        R, H, r = g2_add(t, g2_in(pg, 0), g2_in(pg, 6))
+        pg.output(g2_flat(R) + list(H) + list(r))
+        progs["G2ADD"] = pg
+        pg = RowProg("PSI")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_psi(t, pg, g2_in(pg, 0))))
+        progs["PSI"] = pg
+        pg = RowProg("PSI2")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_psi2(t, pg, g2_in(pg, 0))))
+        progs["PSI2"] = pg
     finally:
         G.Prog = saved
     return progs
@@ -210,6 +311,7 @@ class RowCode:
         self.words, self.n_prods, self.n_lins, self.n_phases, self.ntemp = words, n_prods, n_lins, n_phases, ntemp
 
 
+LBR_NROWS = 64  # lb_row.h: 4 rows per wave, LBR_WAVES 16
 ZERO_SLOT = G.CONST_BASE + G.C_ZERO
 
 
@@ -218,15 +320,52 @@ def _pair(slot, coef):
     return (slot & 0xFFFF) | ((coef & 0xFFFF) << 16)
 
 
+def _live_lins(pg):
+    """the linear tasks whose result is read (by a product, a live task or as an output)"""
+    live = list(pg.lins)
+    while True:
+        used = set(pg.outs)
+        for p in pg.prods:
+            used |= set(p[2].d) | set(p[3].d)
+        for l in live:
+            used |= set(l[3].d)
+        keep = [l for l in live if l[2] in used]
+        if len(keep) == len(live):
+            return keep
+        live = keep
+
+
 def encode(pg):
+    pg.lins = _live_lins(pg)
     nst = max([p[0] for p in pg.prods] + [l[0] for l in pg.lins] + [0])
+    # A level-0 linear task of stage s that neither a product of stage s + 1 nor another linear
+    # task of stage s reads (typically an output) is deferred into stage s + 1's product phase:
+    # it runs on the rows after the products' (header word 1: row offset) with no barrier between
+    # (product phase flag 16), one phase and barrier fewer.
+    def reads(lin, slot):
+        return slot in lin.d
+    deferred = {}
+    if os.environ.get("ROW_NO_DEFER") != "1":
+        for s in range(nst):
+            nxt = [p for p in pg.prods if p[0] == s + 1]
+            if not nxt:
+                continue
+            same = [l for l in pg.lins if l[0] == s]
+            deferred[s + 1] = [l for l in same if l[1] == 0
+                               and not any(reads(p[2], l[2]) or reads(p[3], l[2]) for p in nxt)
+                               and not any(reads(o[3], l[2]) for o in same)]
+    moved = {id(l) for ls in deferred.values() for l in ls}
     phases = []
     for s in range(nst + 1):
         pr = [p for p in pg.prods if p[0] == s]
         if pr:
-            phases.append((0, pr))
-        for v in sorted({l[1] for l in pg.lins if l[0] == s}):
-            phases.append((1, [l for l in pg.lins if l[0] == s and l[1] == v]))
+            dl = deferred.get(s, [])
+            phases.append((0, pr, bool(dl)))
+            if dl:
+                roff = 4 * ((len(pr) + 3) // 4)
+                phases.append((1, dl, roff if roff < LBR_NROWS else 0))
+        for v in sorted({l[1] for l in pg.lins if l[0] == s and id(l) not in moved}):
+            phases.append((1, [l for l in pg.lins if l[0] == s and l[1] == v and id(l) not in moved], 0))
     out = [len(phases), len(pg.outs)] + list(pg.outs)
 
     def pairs(lin, width):
@@ -242,22 +381,25 @@ def encode(pg):
         # product is below 1.4 p without the quotient reduction (only the limb carries run)
         return any(sum(abs(c) for c in l.d.values()) > 16 for l in lins)
 
-    for kind, tasks in phases:
+    for kind, tasks, arg in phases:
         if kind == 0:
             xs, ys = [t[2] for t in tasks], [t[3] for t in tasks]
             nx, ny = max(len(x.d) for x in xs), max(len(y.d) for y in ys)
             flags = (1 if plain(xs) else 0) | (2 if plain(ys) else 0)
             flags |= (4 if reduce(xs) else 0) | (8 if reduce(ys) else 0)
+            flags |= 16 if arg else 0
             out += [kind | (flags << 8) | (len(tasks) << 16), nx | (ny << 16)]
             for t in tasks:
                 out += [t[1]] + pairs(t[2], nx) + pairs(t[3], ny)
         else:
             ls = [t[3] for t in tasks]
             nx = max(len(l.d) for l in ls)
-            out += [kind | (len(tasks) << 16), nx]
+            out += [kind | (len(tasks) << 16), nx | (arg << 16)]
             for t in tasks:
                 out += [t[2]] + pairs(t[3], nx)
-    return RowCode(out, len(pg.prods), len(pg.lins), len(phases), pg.ntemp)
+    code = RowCode(out, len(pg.prods), len(pg.lins), len(phases), pg.ntemp)
+    code.n_barriers = sum(1 for k, _, a in phases if not (k == 0 and a))
+    return code
 
 
 def run_row(words, slots):
@@ -282,7 +424,7 @@ def run_row(words, slots):
         pos += 2
         kind, flags, n = h0 & 0xFF, (h0 >> 8) & 0xFF, h0 >> 16
         nx, ny = h1 & 0xFFFF, h1 >> 16
-        rs = 1 + nx + (ny if kind == 0 else 0)
+        rs = 1 + nx + (ny if kind == 0 else 0)  # (a linear phase's ny: its row offset)
         new = {}
         for k in range(n):
             rec = words[pos + k * rs: pos + (k + 1) * rs]
@@ -300,13 +442,19 @@ def run_row(words, slots):
 
 
 def consts_values():
-    """the CONST slots as field elements (same order as lb_wave.h w_init_consts)"""
+    """the CONST slots as field elements (same order as lb_wave.h w_init_consts, then psi's)"""
     sys.path.insert(0, ROOT)
     from oracle import bls_oracle as o
-    c = [0] * N_CONST
+    c = [0] * N_CONST_ROW
+    xi = (1, 1)
+    cx = o.PSI_CX
+    cy = o.PSI_CY
+    c[C_PSI_CX], c[C_PSI_CX + 1] = cx
+    c[C_PSI_CY], c[C_PSI_CY + 1] = cy
+    c[C_PSI2_CX] = o.f2_mul(cx, o.f2_conj(cx))[0]
+    c[C_PSI2_CY] = o.f2_mul(cy, o.f2_conj(cy))[0]
     c[G.C_B3], c[G.C_B3 + 1] = 12, 12
     c[G.C_INV2] = pow(2, P - 2, P)
-    xi = (1, 1)
     for k in range(1, 6):
         g = o.f2_pow(xi, k * (P - 1) // 6)
         c[G.C_FROB1 + 2 * (k - 1)], c[G.C_FROB1 + 2 * (k - 1) + 1] = g
@@ -352,6 +500,32 @@ def _checks(codes):
         S.update({G.IN_BASE + k: to_row(flat[k]) for k in range(12)})
         got = [from_row(v) for v in run_row(codes["CSQR12"].words, S)]
         assert f12(got) == o.f12_sqr(g), "CSQR12"
+    # G2 point programs against the oracle's group law (affine results)
+    def g2_row_in(Pa):
+        (x0, x1), (y0, y1) = Pa
+        z = (rnd.randrange(1, P), rnd.randrange(P))  # a random Jacobian representative
+        z2 = o.f2_sqr(z)
+        X, Y = o.f2_mul(Pa[0], z2), o.f2_mul(Pa[1], o.f2_mul(z2, z))
+        return [X[0], X[1], Y[0], Y[1], z[0], z[1]]
+
+    def g2_row_out(v):
+        X, Y, Z = (v[0], v[1]), (v[2], v[3]), (v[4], v[5])
+        zi = o.f2_inv(Z)
+        zi2 = o.f2_sqr(zi)
+        return (o.f2_mul(X, zi2), o.f2_mul(Y, o.f2_mul(zi2, zi)))
+    for k in range(2):
+        Pa = o.hash_to_g2(bytes([k, 1]) * 16)
+        Qa = o.hash_to_g2(bytes([k, 2]) * 16)
+        S = dict(base)
+        S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(g2_row_in(Pa) + g2_row_in(Qa))})
+        got = [from_row(v) for v in run_row(codes["G2DBL"].words, S)]
+        assert g2_row_out(got) == o.g2_add(Pa, Pa), "G2DBL"
+        got = [from_row(v) for v in run_row(codes["G2ADD"].words, S)]
+        assert g2_row_out(got[:6]) == o.g2_add(Pa, Qa), "G2ADD"
+        got = [from_row(v) for v in run_row(codes["PSI"].words, S)]
+        assert g2_row_out(got) == o.g2_psi(Pa), "PSI"
+        got = [from_row(v) for v in run_row(codes["PSI2"].words, S)]
+        assert g2_row_out(got) == o.g2_psi(o.g2_psi(Pa)), "PSI2"
     # a few Miller steps against the lone-lane programs' interpreter (values, not limbs)
     Pp = o.sk_to_pk(0x1234567)
     Qq = o.hash_to_g2(b"\x07" * 32)
@@ -368,7 +542,7 @@ def _checks(codes):
         assert got == want, name
 
 
-ORDER = ["MUL12", "SQR12", "CSQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP"]
+ORDER = ["MUL12", "SQR12", "CSQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2"]
 
 
 def const_limbs(v):
@@ -385,7 +559,9 @@ def render(check=True):
              "#pragma once", "#include <stdint.h>", "",
              f"#define LBR_IN {G.IN_BASE}", f"#define LBR_CONST {G.CONST_BASE}", f"#define LBR_TEMP {G.TEMP_BASE}",
              f"#define LBR_C_B3 {G.C_B3}", f"#define LBR_C_INV2 {G.C_INV2}", f"#define LBR_C_FROB1 {G.C_FROB1}",
-             f"#define LBR_C_FROB2 {G.C_FROB2}", f"#define LBR_C_ZERO {G.C_ZERO}", f"#define LBR_N_CONST {N_CONST}",
+             f"#define LBR_C_FROB2 {G.C_FROB2}", f"#define LBR_C_ZERO {G.C_ZERO}", f"#define LBR_N_CONST {N_CONST_ROW}",
+             f"#define LBR_C_PSI_CX {C_PSI_CX}", f"#define LBR_C_PSI_CY {C_PSI_CY}", f"#define LBR_C_PSI2_CX {C_PSI2_CX}",
+             f"#define LBR_C_PSI2_CY {C_PSI2_CY}",
              f"#define LBR_INV_P336 {INV_P336.hex()}  // 2^336 / p, nearest double"]
     image, maxtemp = [], 0
     for name in ORDER:
@@ -398,7 +574,9 @@ def render(check=True):
         image += [0] * (-len(image) % 4)
         if name == "FROB2":
             lines.append(f"#define LBR_PROGS_FE {len(image)}")
-    lines.append(f"#define LBR_PROGS_ALL {len(image)}")
+        if name == "ADD_STEP":
+            lines.append(f"#define LBR_PROGS_ALL {len(image)}")
+    lines.append(f"#define LBR_PROGS_END {len(image)}")
     lines.append(f"#define LBR_MAX_TEMPS {maxtemp}")
     signed = [v - (1 << 32) if v >= (1 << 31) else v for v in image]
     lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_PROGS[{len(image)}] = "
@@ -406,7 +584,7 @@ def render(check=True):
     # constants: the CONST slots in row form, p, -p^-1 mod 2^392, and the conversion factors
     cv = consts_values()
     rows = [const_limbs(v * RP % P) for v in cv]
-    lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_CONST_LIMBS[{N_CONST}][16] = {{"
+    lines.append(f"static __device__ const int32_t __attribute__((aligned(16))) LBR_CONST_LIMBS[{N_CONST_ROW}][16] = {{"
                  + ", ".join("{" + ", ".join(str(x) for x in r + [0, 0]) + "}" for r in rows) + "};")
 
     def arr(name, v, comment):
@@ -427,7 +605,7 @@ def main():
         fh.write(text)
     for name in ORDER:
         c = codes[name]
-        print(f"{name}: {c.n_prods} products, {c.n_phases} phases, {len(c.words)} words")
+        print(f"{name}: {c.n_prods} products, {c.n_phases} phases, {c.n_barriers} barriers, {len(c.words)} words")
     print("wrote", OUT_PATH)
 
 

@@ -7,6 +7,7 @@
 #define LB_KGROUP 99
 __device__ unsigned long long g_ph[64][3];
 __device__ int g_ph_n;
+#ifdef UB_HOOKS
 #define LBR_PHASE_HOOK(ph, kind, n)                                  \
   if (threadIdx.x == 0 && g_ph_n < 64) {                             \
     g_ph[g_ph_n][0] = __builtin_readcyclecounter();                  \
@@ -14,6 +15,17 @@ __device__ int g_ph_n;
     g_ph[g_ph_n][2] = n;                                             \
     g_ph_n++;                                                        \
   }
+// sub-phase points of the first product of a phase (thread 0), after the value v is ready
+#define LBR_SUB_HOOK(tag, v)                                                        \
+  if (threadIdx.x == 0 && g_ph_n < 64) {                                             \
+    asm volatile("" ::"v"(v));                                                       \
+    __builtin_amdgcn_s_waitcnt(0);                                                   \
+    g_ph[g_ph_n][0] = __builtin_readcyclecounter();                                  \
+    g_ph[g_ph_n][1] = 10 + (tag);                                                    \
+    g_ph[g_ph_n][2] = 0;                                                             \
+    g_ph_n++;                                                                        \
+  }
+#endif
 #include "lb_kernels.h"
 
 __device__ __forceinline__ uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
@@ -55,10 +67,38 @@ __global__ void __launch_bounds__(LBR_NT) k_row_ops(int iters, uint64_t* out) {
   const uint64_t t1 = rt();
   if (threadIdx.x == 0) out[0] = t1 - t0;
 }
+// G2 point ops on (1, 1, 1)-filled slots (any values: timing only)
+__device__ void ub_fill_ones(int32_t* S, int dst, int n) {
+  const int t = r_tid();
+  if (t < 16 * n) {
+    int v = 0;
+    for (int i = 0; i < 14; i++) v = (t & 15) == i ? lbr_k::ONE[i] : v;
+    S[16 * (dst + (t >> 4)) + (t & 15)] = v + ((t >> 4) == 3 ? 5 : 0);
+  }
+  r_sync();
+}
+template <int OP>
+__global__ void __launch_bounds__(LBR_NT) k_g2_ops(int iters, uint64_t* out) {
+  LBR_SHARED_N(S, LBR_PROGS_END);
+  r_init(S, LBR_PROGS_END, 0);
+  ub_fill_ones(S, LBR_A(0), 12);
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    if (OP == 0) r_g2_dbl(S, LBR_A(0), LBR_A(0));
+    if (OP == 1) r_g2_add(S, LBR_A(0), LBR_A(0), LBR_A(0) + 6);
+    if (OP == 2) r_exec(S, LBR_G2DBL);
+    if (OP == 3) r_g2_clear_cofactor<true>(S, LBR_A(4), LBR_A(3));
+    if (OP == 4) r_zero_mask(S, 8, [&](int e) { return LBR_A(0) + e; });
+    if (OP == 5) r_out(S, LBR_G2DBL, 0, 6, LBR_IN);
+  }
+  r_sync();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+}
 template <int OP>
 __global__ void __launch_bounds__(LBR_NT) k_phases(unsigned long long* out) {
-  LBR_SHARED(S);
-  r_init(S);
+  LBR_SHARED_N(S, LBR_PROGS_END);
+  r_init(S, LBR_PROGS_END, 0);
   r_set_one(S, LBR_A(0));
   if (threadIdx.x == 0) g_ph_n = 0;
   r_copy(S, LBR_IN, LBR_A(0), 24);
@@ -67,6 +107,9 @@ __global__ void __launch_bounds__(LBR_NT) k_phases(unsigned long long* out) {
   if (OP == 0) r_exec(S, LBR_CSQR12);
   if (OP == 1) r_exec(S, LBR_MUL12);
   if (OP == 2) r_exec(S, LBR_DBL_STEP);
+  if (OP == 3) r_exec(S, LBR_G2DBL);
+  if (OP == 4) r_exec(S, LBR_G2ADD);
+  if (OP == 5) r_exec(S, LBR_ADD_STEP);
   const unsigned long long t1 = __builtin_readcyclecounter();
   if (threadIdx.x == 0) { out[0] = t0; out[1] = t1; }
 }
@@ -217,8 +260,11 @@ int main() {
   {
     unsigned long long* dd;
     hipMalloc(&dd, 64);
-    const char* nm[3] = {"CSQR12", "MUL12", "DBL_STEP"};
-    for (int op = 0; op < 3; op++) {
+    const char* nm[6] = {"CSQR12", "MUL12", "DBL_STEP", "G2DBL", "G2ADD", "ADD_STEP"};
+    for (int op = 0; op < 6; op++) {
+      if (op == 3) hipLaunchKernelGGL(k_phases<3>, dim3(1), dim3(LBR_NT), 0, 0, dd);
+      if (op == 4) hipLaunchKernelGGL(k_phases<4>, dim3(1), dim3(LBR_NT), 0, 0, dd);
+      if (op == 5) hipLaunchKernelGGL(k_phases<5>, dim3(1), dim3(LBR_NT), 0, 0, dd);
       if (op == 0) hipLaunchKernelGGL(k_phases<0>, dim3(1), dim3(LBR_NT), 0, 0, dd);
       if (op == 1) hipLaunchKernelGGL(k_phases<1>, dim3(1), dim3(LBR_NT), 0, 0, dd);
       if (op == 2) hipLaunchKernelGGL(k_phases<2>, dim3(1), dim3(LBR_NT), 0, 0, dd);
@@ -230,10 +276,20 @@ int main() {
       hipMemcpyFromSymbol(&np, HIP_SYMBOL(g_ph_n), 4);
       printf("%s: %llu cycles total;", nm[op], tt[1] - tt[0]);
       unsigned long long prev = tt[0];
-      for (int i = 0; i < np; i++) { printf(" %s%llu:%llu", ph[i][1] ? "L" : "P", ph[i][2], ph[i][0] - prev); prev = ph[i][0]; }
+      for (int i = 0; i < np; i++) {
+        if (ph[i][1] >= 10) printf(" s%llu:%llu", ph[i][1] - 10, ph[i][0] - prev);
+        else printf(" %s%llu:%llu |", ph[i][1] ? "L" : "P", ph[i][2], ph[i][0] - prev);
+        prev = ph[i][0];
+      }
       printf("\n");
     }
   }
+  run("row G2 dbl", [&](int n) { hipLaunchKernelGGL(k_g2_ops<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row G2 add", [&](int n) { hipLaunchKernelGGL(k_g2_ops<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row G2DBL exec only", [&](int n) { hipLaunchKernelGGL(k_g2_ops<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row zero mask (8)", [&](int n) { hipLaunchKernelGGL(k_g2_ops<4>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row out (6)", [&](int n) { hipLaunchKernelGGL(k_g2_ops<5>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
+  run("row clear cofactor", [&](int n) { hipLaunchKernelGGL(k_g2_ops<3>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 2);
   run("wave SQR12 (64 thr)", [&](int n) { hipLaunchKernelGGL(k_wave_ops<0>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
   run("wave MUL12", [&](int n) { hipLaunchKernelGGL(k_wave_ops<1>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
   return 0;
