@@ -694,8 +694,7 @@ __global__ void __launch_bounds__(LBR_NT) k_hash_finish_row(uint32_t n, const ui
     r_import_staged(S, Q0, 12);
   }
   r_copy(S, LBR_A(5), Q0, 12);  // Q0, Q1 kept for a recomputation
-  r_g2_add_fast(S, Q0, Q0, Q1);
-  r_g2_clear_cofactor<true>(S, H, Q0);
+  r_run(S, &LBR_OPS_HASH, LBR_OPS_HASH.n);  // Q0 + Q1, cofactor clearing into H (fast path)
   // Z = 0 (or `careful`, LB_HASH_ROW_CAREFUL for the tests): again with the tests
   if (r_zero_mask(S, 2, [&](int e) { return H + 4 + e; }) == 3 || careful) {
     r_copy(S, Q0, LBR_A(5), 12);

@@ -282,7 +282,7 @@ __device__ __forceinline__ void r_prefetch(const lds_i32* prog, int pos, int h0,
     offB = 9;
     nB = nx - 8;
   }
-  t = min(t, n - 1);  // idle rows read a valid record (unused)
+  if (t >= n) return;  // an idle row (its words are not used)
   const lds_i32* rec = prog + pos + t * rs;
   p.dst = rec[0];
   LB_UNROLL for (int j = 0; j < 8; j++) p.w[j] = rec[1 + min(j, nA - 1)];
@@ -333,10 +333,14 @@ __device__ void r_exec_tail(lds_i32* S, const lds_i32* prog, int pos, int h0, in
   }
 }
 
+#ifndef LBR_EXEC_ATTR
+#define LBR_EXEC_ATTR __attribute__((noinline))
+#endif
 #ifndef LBR_EXEC_V1
 // Run one program (offset `off` in the image): inputs already in IN, outputs left in the temps
-// the header lists.
-__device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
+// the header lists.  r_exec_inl is inlined once into r_run's loop (lb_row.h, end): a call of the
+// out-of-line r_exec costs ~0.9 us of callee-saved scratch round trips, on the order of a phase.
+__device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) {
   lds_i32* S = r_lds(S_generic);
   const lds_i32* prog = r_progs(S_generic) + off;
   const int k = r_limb(), row = r_row(), pk = r_plimb(k);
@@ -401,6 +405,7 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
     h1 = nh1;
   }
 }
+__device__ LBR_EXEC_ATTR void r_exec(int32_t* S_generic, int off) { r_exec_inl(S_generic, off); }
 #else
 __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
   lds_i32* S = r_lds(S_generic);
@@ -470,6 +475,7 @@ __device__ __attribute__((noinline)) void r_exec(int32_t* S_generic, int off) {
 #endif
   }
 }
+__device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) { r_exec(S_generic, off); }
 #endif  // LBR_EXEC_V1
 
 // ---------------------------------------------------------------- element moves (limb-parallel)
@@ -706,6 +712,183 @@ __device__ bool r_eq(int32_t* S_generic, int a, int b) {
   r_sync();
   return r == 0;
 }
+// ---------------------------------------------------------------- op lists (one r_exec site)
+// A fixed sequence of Fp12 / G2 / Miller-step operations as a table of (kind, dst, a, b) words
+// built at compile time (constexpr), run by r_run: one loop with the interpreter inlined once, so
+// the final exponentiation's ~360 programs, a Miller loop's 68 steps and the cofactor clearing's
+// ~140 point operations pay no call overhead per program.
+enum {
+  RK_MUL,    // dst = a b (Fp12)
+  RK_SQR,    // dst = a^2
+  RK_CSQR,   // dst = a^2, a cyclotomic
+  RK_FROB,   // dst = a^p
+  RK_FROB2,  // dst = a^(p^2)
+  RK_G2DBL,  // dst = 2a (6-slot Jacobian G2)
+  RK_G2ADD,  // dst = a + b (no exceptional cases)
+  RK_PSI,    // dst = psi(a)
+  RK_PSI2,   // dst = psi^2(a)
+  RK_MLDBL,  // Miller doubling step: f = dst (12), T at LBR_PT + 6, P at LBR_PT
+  RK_MLADD,  // Miller addition step: the same with Q at LBR_PT + 2
+  RK_CONJ,   // dst = conj(a) (Fp12)
+  RK_COPY,   // dst[0, b) = a[0, b)
+  RK_G2NEG,  // a = -a (G2)
+};
+#define LBR_MAX_OPS 400
+struct r_opl {
+  int n = 0;
+  int w[2 * LBR_MAX_OPS] = {};
+  constexpr void op(int kind, int dst, int a, int b = 0) {
+    w[2 * n] = kind | (dst << 16);
+    w[2 * n + 1] = a | (b << 16);
+    n++;
+  }
+  // dst = a^|x| (a cyclotomic, dst != a)
+  constexpr void pow_xabs(int dst, int a) {
+    op(RK_COPY, dst, a, 12);
+    for (int i = 62; i >= 0; i--) {
+      op(RK_CSQR, dst, dst);
+      if ((LB_X_ABS >> i) & 1ull) op(RK_MUL, dst, dst, a);
+    }
+  }
+  // dst = [|x|] a (G2, dst != a)
+  constexpr void g2_mul_xabs(int dst, int a) {
+    op(RK_COPY, dst, a, 6);
+    for (int i = 62; i >= 0; i--) {
+      op(RK_G2DBL, dst, dst);
+      if ((LB_X_ABS >> i) & 1ull) op(RK_G2ADD, dst, dst, a);
+    }
+  }
+};
+// r_final_exp after the inversion (Y0 = f^-1): the chain of lb_pairing.h final_exponentiation
+constexpr r_opl r_ops_fe_tail(int dst, int f) {
+  r_opl o;
+  const int T0 = LBR_A(1), A0 = LBR_A(2), B0 = LBR_A(3), C0 = LBR_A(4), X0 = LBR_A(5), Y0 = LBR_A(6);
+  o.op(RK_CONJ, X0, f);
+  o.op(RK_MUL, T0, X0, Y0);
+  o.op(RK_FROB2, X0, T0);
+  o.op(RK_MUL, T0, X0, T0);
+  o.pow_xabs(X0, T0);
+  o.op(RK_MUL, X0, X0, T0);
+  o.op(RK_CONJ, A0, X0);
+  o.pow_xabs(X0, A0);
+  o.op(RK_MUL, X0, X0, A0);
+  o.op(RK_CONJ, A0, X0);
+  o.pow_xabs(X0, A0);
+  o.op(RK_CONJ, X0, X0);
+  o.op(RK_FROB, Y0, A0);
+  o.op(RK_MUL, B0, X0, Y0);
+  o.pow_xabs(X0, B0);
+  o.pow_xabs(C0, X0);
+  o.op(RK_FROB2, X0, B0);
+  o.op(RK_MUL, C0, C0, X0);
+  o.op(RK_CONJ, X0, B0);
+  o.op(RK_MUL, C0, C0, X0);
+  o.op(RK_CSQR, X0, T0);
+  o.op(RK_MUL, X0, X0, T0);
+  o.op(RK_MUL, dst, C0, X0);
+  return o;
+}
+// the Miller loop's steps into area dst (after r_miller's setup, before its final conjugation)
+constexpr r_opl r_ops_miller(int dst) {
+  r_opl o;
+  for (int i = 62; i >= 0; i--) {
+    o.op(RK_MLDBL, dst, 0);
+    if ((LB_X_ABS >> i) & 1ull) o.op(RK_MLADD, dst, 0);
+  }
+  return o;
+}
+// Q0 + Q1 (slots q .. q + 11), then h_eff (Q0 + Q1) via psi into dst (as r_g2_clear_cofactor<true>)
+constexpr r_opl r_ops_hash_finish(int dst, int q) {
+  r_opl o;
+  const int T1 = LBR_A(0), T3 = LBR_A(0) + 6, T2 = LBR_A(1), X = LBR_A(1) + 6, W = LBR_A(2);
+  const int p = q;
+  o.op(RK_G2ADD, p, q, q + 6);
+  o.g2_mul_xabs(T1, p);
+  o.op(RK_G2NEG, T1, T1);
+  o.op(RK_G2DBL, T3, p);
+  o.op(RK_PSI2, T3, T3);
+  o.op(RK_PSI, T2, p);
+  o.op(RK_COPY, W, T2, 6);
+  o.op(RK_G2NEG, W, W);
+  o.op(RK_G2ADD, T3, T3, W);
+  o.op(RK_G2ADD, T2, T2, T1);
+  o.g2_mul_xabs(X, T2);
+  o.op(RK_G2NEG, X, X);
+  o.op(RK_G2ADD, T3, T3, X);
+  o.op(RK_G2NEG, T1, T1);
+  o.op(RK_G2ADD, T3, T3, T1);
+  o.op(RK_COPY, W, p, 6);
+  o.op(RK_G2NEG, W, W);
+  o.op(RK_G2ADD, dst, T3, W);
+  return o;
+}
+static __device__ const r_opl LBR_OPS_FE_A0 = r_ops_fe_tail(LBR_A(0), LBR_A(0));
+static __device__ const r_opl LBR_OPS_ML_A0 = r_ops_miller(LBR_A(0));
+static __device__ const r_opl LBR_OPS_ML_A7 = r_ops_miller(LBR_A(7));
+static __device__ const r_opl LBR_OPS_HASH = r_ops_hash_finish(LBR_A(4), LBR_A(3));
+static_assert(r_ops_fe_tail(LBR_A(0), LBR_A(0)).n <= LBR_MAX_OPS && r_ops_hash_finish(LBR_A(4), LBR_A(3)).n <= LBR_MAX_OPS,
+              "lb_row.h: op list size");
+
+// run ops[0, n): every program through one inlined interpreter
+__device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl* ops, int n) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row(), t = r_tid();
+  const int PP = LBR_PT, QQ = LBR_PT + 2, TT = LBR_PT + 6;
+  for (int i = 0; i < n; i++) {
+    const int w0 = __builtin_amdgcn_readfirstlane(ops->w[2 * i]), w1 = __builtin_amdgcn_readfirstlane(ops->w[2 * i + 1]);
+    const int kind = w0 & 0xffff, dst = w0 >> 16, a = w1 & 0xffff, b = w1 >> 16;
+    if (kind == RK_CONJ) {
+      r_conj(S_generic, dst, a);
+      continue;
+    }
+    if (kind == RK_COPY) {
+      r_copy(S_generic, dst, a, b);
+      continue;
+    }
+    if (kind == RK_G2NEG) {  // in place (dst == a)
+      if (t < 32) S[16 * (a + 2) + t] = -S[16 * (a + 2) + t];
+      r_sync();
+      continue;
+    }
+    int prog, na, nb, nout;
+    switch (kind) {
+      case RK_MUL: prog = LBR_MUL12; na = 12; nb = 12; nout = 12; break;
+      case RK_SQR: prog = LBR_SQR12; na = 12; nb = 0; nout = 12; break;
+      case RK_CSQR: prog = LBR_CSQR12; na = 12; nb = 0; nout = 12; break;
+      case RK_FROB: prog = LBR_FROB; na = 12; nb = 0; nout = 12; break;
+      case RK_FROB2: prog = LBR_FROB2; na = 12; nb = 0; nout = 12; break;
+      case RK_G2DBL: prog = LBR_G2DBL; na = 6; nb = 0; nout = 6; break;
+      case RK_G2ADD: prog = LBR_G2ADD; na = 6; nb = 6; nout = 6; break;
+      case RK_PSI: prog = LBR_PSI; na = 6; nb = 0; nout = 6; break;
+      case RK_PSI2: prog = LBR_PSI2; na = 6; nb = 0; nout = 6; break;
+      case RK_MLDBL: prog = LBR_DBL_STEP; na = 12; nb = 0; nout = 18; break;
+      default: prog = LBR_ADD_STEP; na = 12; nb = 0; nout = 18; break;  // RK_MLADD
+    }
+    const bool ml = kind >= RK_MLDBL;
+    const int src_a = ml ? dst : a;
+    // inputs into IN (sources never in IN: one barrier)
+    const int nin = ml ? (kind == RK_MLDBL ? 20 : 24) : na + nb;
+    for (int e = row; e < nin; e += LBR_NROWS) {
+      int sl;
+      if (e < na) sl = src_a + e;
+      else if (!ml) sl = b + e - na;
+      else if (e < 18) sl = TT + e - 12;
+      else if (kind == RK_MLDBL) sl = PP + e - 18;
+      else sl = e < 22 ? QQ + e - 18 : PP + e - 22;
+      S[16 * (LBR_IN + e) + k] = S[16 * sl + k];
+    }
+    r_sync();
+    r_exec_inl(S_generic, prog);
+    // outputs (temps) to dst (and T for the Miller steps)
+    const lds_i32* pr = r_progs(S_generic) + prog;
+    for (int e = row; e < nout; e += LBR_NROWS) {
+      const int d = e < 12 || !ml ? dst + e : TT + e - 12;
+      S[16 * d + k] = S[16 * pr[2 + e] + k];
+    }
+    r_sync();
+  }
+}
+
 // dst = a^-1 by norms down to Fp2 (lb_wave.h w_inv): one Fp inversion on thread 0 (inline EEA)
 __device__ void r_inv(int32_t* S, int dst, int a, int t1, int t2, int t3) {
   __shared__ fp nv[2];
@@ -740,6 +923,12 @@ __device__ void r_pow_xabs(int32_t* S, int dst, int a) {
 __device__ void r_final_exp(int32_t* S, int dst, int f) {
   const int T0 = LBR_A(1), A0 = LBR_A(2), B0 = LBR_A(3), C0 = LBR_A(4), X0 = LBR_A(5), Y0 = LBR_A(6);
   r_inv(S, Y0, f, A0, B0, C0);
+#ifndef LBR_NO_OPLIST
+  if (dst == LBR_A(0) && f == LBR_A(0)) {
+    r_run(S, &LBR_OPS_FE_A0, LBR_OPS_FE_A0.n);
+    return;
+  }
+#endif
   r_conj(S, X0, f);
   r_mul(S, T0, X0, Y0);
   r_frob2(S, X0, T0);
@@ -784,6 +973,13 @@ __device__ void r_miller(int32_t* S_generic, int dst) {
     }
     r_sync();
   }
+#ifndef LBR_NO_OPLIST
+  if (dst == LBR_A(0) || dst == LBR_A(7)) {
+    r_run(S_generic, dst == LBR_A(0) ? &LBR_OPS_ML_A0 : &LBR_OPS_ML_A7, LBR_OPS_ML_A0.n);
+    r_conj(S_generic, dst, dst);
+    return;
+  }
+#endif
   for (int i = 62; i >= 0; i--) {
     r_gather(S_generic, LBR_IN, 20, [&](int e) { return e < 12 ? dst + e : (e < 18 ? TT + e - 12 : PP + e - 18); });
     r_exec(S_generic, LBR_DBL_STEP);

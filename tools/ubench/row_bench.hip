@@ -90,6 +90,47 @@ __global__ void __launch_bounds__(LBR_NT) k_g2_ops(int iters, uint64_t* out) {
     if (OP == 3) r_g2_clear_cofactor<true>(S, LBR_A(4), LBR_A(3));
     if (OP == 4) r_zero_mask(S, 8, [&](int e) { return LBR_A(0) + e; });
     if (OP == 5) r_out(S, LBR_G2DBL, 0, 6, LBR_IN);
+    if (OP == 6) r_run(S, &LBR_OPS_HASH, LBR_OPS_HASH.n);
+  }
+  r_sync();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+}
+// synthetic one-phase programs written over the image at offset 0: the cost of a phase's parts
+template <int V>
+__global__ void __launch_bounds__(LBR_NT) k_synth(int iters, uint64_t* out) {
+  LBR_SHARED(S);
+  r_init(S);
+  ub_fill_ones(S, LBR_A(0), 12);
+  if (threadIdx.x == 0) {
+    lds_i32* P = r_lds(S) + LBR_SLOT_WORDS + LBR_MISC;
+    int w = 0;
+    const int A0 = LBR_A(0);
+    auto pair = [&](int slot, int c) { return (slot & 0xffff) | (c << 16); };
+    const int nprod = V == 6 ? 16 : (V == 8 ? 64 : 1);
+    P[w++] = 1;  // phases
+    P[w++] = 0;  // outputs
+    if (V <= 2 || V == 6 || V == 8) {
+      const int nt = V == 0 || V == 6 || V == 8 ? 1 : 8, flags = V == 0 || V == 6 || V == 8 ? 3 : (V == 2 ? 12 : 0);
+      P[w++] = 0 | (flags << 8) | (nprod << 16);
+      P[w++] = nt | (nt << 16);
+      for (int t = 0; t < nprod; t++) {
+        P[w++] = LBR_TEMP + t;
+        for (int j = 0; j < 2 * nt; j++) P[w++] = pair(A0 + (j % 12), 1);
+      }
+    } else if (V == 3 || V == 4) {
+      const int nt = V == 3 ? 1 : 8;
+      P[w++] = 1 | (1 << 16);
+      P[w++] = nt;
+      P[w++] = LBR_TEMP;
+      for (int j = 0; j < nt; j++) P[w++] = pair(A0 + j, 1);
+    }
+  }
+  r_sync();
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    if (V == 7) r_sync();
+    else r_exec(S, 0);
   }
   r_sync();
   const uint64_t t1 = rt();
@@ -284,12 +325,21 @@ int main() {
       printf("\n");
     }
   }
+  run("synth P1 plain", [&](int n) { hipLaunchKernelGGL(k_synth<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth P1 8+8 terms", [&](int n) { hipLaunchKernelGGL(k_synth<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth P1 8+8 reduce", [&](int n) { hipLaunchKernelGGL(k_synth<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth L1 1 term", [&](int n) { hipLaunchKernelGGL(k_synth<3>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth L1 8 terms", [&](int n) { hipLaunchKernelGGL(k_synth<4>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth P16 plain", [&](int n) { hipLaunchKernelGGL(k_synth<6>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth P64 plain", [&](int n) { hipLaunchKernelGGL(k_synth<8>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+  run("synth barrier", [&](int n) { hipLaunchKernelGGL(k_synth<7>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("row G2 dbl", [&](int n) { hipLaunchKernelGGL(k_g2_ops<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row G2 add", [&](int n) { hipLaunchKernelGGL(k_g2_ops<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row G2DBL exec only", [&](int n) { hipLaunchKernelGGL(k_g2_ops<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row zero mask (8)", [&](int n) { hipLaunchKernelGGL(k_g2_ops<4>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row out (6)", [&](int n) { hipLaunchKernelGGL(k_g2_ops<5>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row clear cofactor", [&](int n) { hipLaunchKernelGGL(k_g2_ops<3>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 2);
+  run("row hash finish op list", [&](int n) { hipLaunchKernelGGL(k_g2_ops<6>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 2);
   run("wave SQR12 (64 thr)", [&](int n) { hipLaunchKernelGGL(k_wave_ops<0>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
   run("wave MUL12", [&](int n) { hipLaunchKernelGGL(k_wave_ops<1>, dim3(1), dim3(64), 0, 0, n, d); }, 200);
   return 0;
