@@ -971,6 +971,25 @@ LB_HD bool fp2_sqrt_i(fp2& out, const fp2& a) {
   return fp2_eq(fp2_sqr(out), a);
 }
 LB_NI bool fp2_sqrt(fp2& out, fp2 a) { return fp2_sqrt_i(out, a); }
+// the same with the two exponentiations by pow(x, exponent words, top bit) (k_hash_map_row: on a row)
+template <class Pow>
+LB_HD bool fp2_sqrt_p(fp2& out, const fp2& a, Pow pow) {
+  const fp norm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  const fp alpha = pow(norm, LB_EXP_SQRT, 378);
+  const fp inv2 = fp_load(LB_INV2);
+  const fp d1 = fp_mul(fp_add(a.c0, alpha), inv2);
+  const fp d2 = fp_mul(fp_sub(a.c0, alpha), inv2);
+  const fp delta = fp_select(fp_is_zero(d1), d2, d1);
+  const fp z = pow(delta, LB_EXP_ISQRT, 378);
+  const fp s = fp_mul(delta, z);
+  const bool delta_qr = fp_eq(fp_sqr(s), delta);
+  fp t = fp_mul(z, inv2);
+  if (!delta_qr) t = fp_neg(t);
+  const fp q = fp_mul(a.c1, t);
+  out.c0 = fp_select(delta_qr, s, q);
+  out.c1 = fp_select(delta_qr, q, s);
+  return fp2_eq(fp2_sqr(out), a);
+}
 
 // RFC 9380 sgn0 for Fp2 (on canonical values)
 LB_HD uint32_t fp2_sgn0(const fp2& a) {

@@ -429,7 +429,10 @@ __device__ __forceinline__ bool fp_is_square_i(const fp& a) {
     if (zero) return false;
   }
 }
-// map_to_curve_g2 (SSWU + 3-isogeny, lb_h2c.h) with the inline pieces above
+// map_to_curve_g2 (SSWU + 3-isogeny, lb_h2c.h) with the inline pieces above; ROW: the square
+// root's two exponentiations on the lane's 16-lane row (r1_pow_const; every lane of the row runs
+// the same item)
+template <bool ROW = false>
 __device__ __forceinline__ g2j map_to_curve_g2_i(const fp2& u) {
   const fp2 A = fp2_load(LB_SSWU_A), B = fp2_load(LB_SSWU_B), Z = fp2_load(LB_SSWU_Z);
   const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
@@ -443,7 +446,10 @@ __device__ __forceinline__ g2j map_to_curve_g2_i(const fp2& u) {
   const bool sq1 = fp_is_square_i(fp_add(fp_sqr(gx1.c0), fp_sqr(gx1.c1)));
   const fp2 x = fp2_select(sq1, x1, x2);
   fp2 y;
-  fp2_sqrt_i<true>(y, fp2_select(sq1, gx1, gx2));
+  if constexpr (ROW)
+    fp2_sqrt_p(y, fp2_select(sq1, gx1, gx2), [](const fp& a, const uint32_t* e, int top) { return r1_pow_const(a, e, top); });
+  else
+    fp2_sqrt_i<true>(y, fp2_select(sq1, gx1, gx2));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   const fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
   const fp2 xn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_XNUM3), xxx), fp2_mul(fp2_load(LB_ISO_XNUM2), xx)),
@@ -482,6 +488,28 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32
     LB_UNROLL for (int k = 0; k < 4; k++) M[4 * i + k] = __builtin_bswap32(w[k]);  // big-endian words
   }
   soa_st(q, 2 * n, which * n + u, map_to_curve_g2_i(hash_to_field_u(M, (int)which)));
+}
+#endif  // LB_KG
+// The same with 16 lanes per field element (4 per wave): the lanes of a row run the same item and
+// share its square roots' exponentiations as row products (lb_row.h r1_pow_const), for batches
+// with few distinct roots on a device running alone (latency: 1.5 -> ~0.6 ms per call).
+#if LB_KG(13)
+__global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, const uint32_t* __restrict__ uniq_set,
+                                                     const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
+  const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 4;
+  if (blockIdx.x * 4 >= 2 * nu) return;  // (whole wave)
+  const uint32_t tc = t < 2 * nu ? t : 2 * nu - 1;  // rows past the end recompute the last item
+  const uint32_t which = tc < nu ? 0u : 1u;
+  const uint32_t u = which ? tc - nu : tc;
+  const uint4* m4 = reinterpret_cast<const uint4*>(msgs + (size_t)32 * uniq_set[u]);
+  uint32_t M[8];
+  LB_UNROLL for (int i = 0; i < 2; i++) {
+    const uint4 v = m4[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    LB_UNROLL for (int k = 0; k < 4; k++) M[4 * i + k] = __builtin_bswap32(w[k]);
+  }
+  const g2j r = map_to_curve_g2_i<true>(hash_to_field_u(M, (int)which));
+  if (t < 2 * nu && (threadIdx.x & 15) == 0) soa_st(q, 2 * n, which * n + u, r);
 }
 #endif  // LB_KG
 

@@ -712,6 +712,77 @@ __device__ bool r_eq(int32_t* S_generic, int a, int b) {
   r_sync();
   return r == 0;
 }
+// ---------------------------------------------------------------- one-row exponentiation
+// An Fp exponentiation by a constant on one 16-lane row of a wave, every lane of the row holding
+// the same fp (the four rows of a wave: four independent items): the chain's products are row
+// products (rp_mul, ~0.45 us each, issue-bound on its 64-bit MADs) with the operand replicated
+// by DPP row broadcasts -- no LDS, no barriers -- instead of lone-lane products (~1.1 us).  The
+// square roots of hash_to_G2's SSWU map use it for small batches (k_hash_map_row).
+__device__ __forceinline__ int r1_sqr(int v, int k) {
+  int x[14];
+  r_rep(v, x);
+  return rp_mul(x, v, k);
+}
+__device__ __forceinline__ int r1_mul(int v, int w, int k) {
+  int x[14];
+  r_rep(v, x);
+  return rp_mul(x, w, k);
+}
+// this lane's limb of a * 2^8 (= a's value in R'-form: a R 2^8 = a R')
+__device__ __forceinline__ int r1_import(const fp& a, int k) {
+  int v = 0;
+  LB_UNROLL for (int i = 0; i < 14; i++) {
+    const int li = i == 0 ? (int)((a.v[0] << 8) & LBR_M28) : (int)lb_bits28(a.v, 28 * i - 8);
+    v = k == i ? li : v;
+  }
+  return v;
+}
+// a row value (R'-form) -> canonical fp (R-form) in every lane of the row
+__device__ __forceinline__ fp r1_export(int v, int k) {
+  const int y = rp_mul(r_cx_const<14>{lbr_k::K_EXPORT}, k < 14 ? v : 0, k);
+  int l[14];
+  r_rep(y, l);
+  return r_canon(l);
+}
+template <int NT>
+__device__ __forceinline__ int r1_sel(const int (&t)[NT], uint32_t i) {
+  int r = t[0];
+  LB_UNROLL for (int c = 1; c < NT; c++) r = i == (uint32_t)c ? t[c] : r;
+  return r;
+}
+// a^e (e: top_bit + 1 bits, a constant), 4-bit windows over odd powers as fp_pow_const_28
+__device__ fp r1_pow_const(const fp& a, const uint32_t* e, int top_bit) {
+  const int k = r_limb();
+  int tab[8];
+  tab[0] = r1_import(a, k);
+  const int a2 = r1_sqr(tab[0], k);
+  LB_UNROLL for (int c = 1; c < 8; c++) tab[c] = r1_mul(tab[c - 1], a2, k);
+  auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
+  int r = tab[0];
+  bool first = true;
+  int i = top_bit;
+  while (i >= 0) {
+    if (!bit(i)) {
+      if (!first) r = r1_sqr(r, k);
+      i--;
+      continue;
+    }
+    int j = i - 3 > 0 ? i - 3 : 0;
+    while (!bit(j)) j++;
+    uint32_t val = 0;
+    for (int c = i; c >= j; c--) val = (val << 1) | bit(c);
+    if (first) {
+      r = r1_sel(tab, val >> 1);
+      first = false;
+    } else {
+      for (int c = i; c >= j; c--) r = r1_sqr(r, k);
+      r = r1_mul(r, r1_sel(tab, val >> 1), k);
+    }
+    i = j - 1;
+  }
+  return r1_export(r, k);
+}
+
 // ---------------------------------------------------------------- op lists (one r_exec site)
 // A fixed sequence of Fp12 / G2 / Miller-step operations as a table of (kind, dst, a, b) words
 // built at compile time (constexpr), run by r_run: one loop with the interpreter inlined once, so
