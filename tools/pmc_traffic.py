@@ -21,17 +21,17 @@ import sys
 STAGES = {
     "decode_sigs": ["k_decompress_sigs", "k_sig_subgroup", "k_sig_subgroup_g8", "k_job_status"],
     "dedup": ["k_msg_insert", "k_msg_count", "k_msg_scatter"],
-    "hash_map": ["k_hash_map"],
-    "hash_finish": ["k_hash_finish", "k_hash_finish_g8"],
+    "hash_map": ["k_hash_map", "k_hash_map_row"],
+    "hash_finish": ["k_hash_finish", "k_hash_finish_g8", "k_hash_finish_row"],
     "pk_chunks": ["k_pk_chunks", "k_pk_chunks_idx"],
     "pk_blind": ["k_pk_blind"],
     "sig_msm": ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce", "k_msm_buckets_g8",
                 "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind", "k_sig_blind_g8", "k_g2_sum64"],
-    "group_sum": ["k_gsum_chunks", "k_gsum_final"],
-    "miller": ["k_miller_g8", "k_miller_lane", "k_miller_wave"],
-    "tree_up_P": ["k_tree_up_U"],
-    "ml_S": ["k_ml_S"],
-    "root_check": ["k_root_check"],
+    "group_sum": ["k_chunk_fill", "k_gsum_chunks", "k_gsum_tree", "k_gsum_final"],
+    "miller": ["k_miller_g8", "k_miller_lane", "k_miller_wave", "k_miller_row"],
+    "tree_up_P": ["k_tree_up_U", "k_tree_up_row"],
+    "ml_S": ["k_ml_S", "k_ml_S_row"],
+    "root_check": ["k_root_check", "k_root_check_row"],
 }
 
 
