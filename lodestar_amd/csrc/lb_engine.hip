@@ -161,7 +161,7 @@ struct lb_engine {
   uint32_t miller_wave_max = 2048;
   // ... and up to this many roots (tree nodes of a level) on the row engine (lb_row.h: one 16-wave
   // workgroup per item, the products split over 16-lane rows; latency).  LB_ROW_MAX.
-  uint32_t row_max = 8;
+  uint32_t row_max = 256;
   int miller_form = 0;  // 0 by load, 1 lane, 2 g8
   // one-lane Miller loops with f and a temporary in LDS (two waves per CU) up to this many roots,
   // f alone in LDS (one wave per SIMD) above: LB_MILLER_LDS3_MAX (lb_kernels.h k_miller_lane)
@@ -169,8 +169,10 @@ struct lb_engine {
   // ... and hash_to_G2's cofactor clearing with 8 lanes per root (k_hash_finish_g8).  LB_HASH_G8_MAX.
   uint32_t hash_g8_max = 2048;
   // ... and with a workgroup per root on the row engine while the device is alone.  LB_HASH_ROW_MAX.
-  uint32_t hash_row_max = 16;
+  uint32_t hash_row_max = 256;
   uint32_t hash_row_careful = 0;  // LB_HASH_ROW_CAREFUL=1: the exceptional-case path always (tests)
+  // ... and the signature decode's square roots on rows up to this many sets.  LB_DEC_ROW_MAX.
+  uint32_t dec_row_max = 4096;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
   uint32_t subgroup_g8_max = 4096;
   // ... and S = sum r_i sig_i by per-set 8-lane scalar multiplications + trees instead of the
@@ -393,6 +395,7 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* mf = getenv("LB_MILLER_FORM")) e->miller_form = !strcmp(mf, "lane") ? 1 : !strcmp(mf, "g8") ? 2 : 0;
   if (const char* hg = getenv("LB_HASH_G8_MAX")) e->hash_g8_max = (uint32_t)strtoul(hg, nullptr, 10);
   if (const char* hr = getenv("LB_HASH_ROW_MAX")) e->hash_row_max = (uint32_t)strtoul(hr, nullptr, 10);
+  if (const char* dr = getenv("LB_DEC_ROW_MAX")) e->dec_row_max = (uint32_t)strtoul(dr, nullptr, 10);
   if (const char* hc = getenv("LB_HASH_ROW_CAREFUL")) e->hash_row_careful = (uint32_t)strtoul(hc, nullptr, 10);
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
@@ -909,9 +912,14 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // signatures: decoded while s1 groups and hashes the messages
     {
       stage_scope sc(e, ST_DECODE, s2);
-      hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
-                         b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
-                         e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      if (n <= e->dec_row_max && e->alone && e->row_fe)
+        hipLaunchKernelGGL(k_decompress_sigs_row, dim3((n + 3) / 4), dim3(64), 0, s2, n, b->d_sigs.as<uint8_t>(),
+                           b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
+                           e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      else
+        hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
+                           b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
+                           e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
       // (8 lanes per signature also for a slot while the device is otherwise idle ran slower:
       // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
       if (n <= e->subgroup_g8_max)

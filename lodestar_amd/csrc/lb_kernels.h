@@ -490,6 +490,41 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_hash_map(uint32_t n, uint32
   soa_st(q, 2 * n, which * n + u, map_to_curve_g2_i(hash_to_field_u(M, (int)which)));
 }
 #endif  // LB_KG
+// k_decompress_sigs with 16 lanes per signature (4 per wave): every lane of a row decodes the
+// same signature and the square root's exponentiations run as row products (r1_pow_const), for
+// small batches on a device running alone.
+#if LB_KG(13)
+__global__ void __launch_bounds__(64) k_decompress_sigs_row(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                            const uint32_t* __restrict__ sig_sizes,
+                                                            uint32_t* __restrict__ sig_aff, uint4* __restrict__ sig_aos,
+                                                            uint32_t* __restrict__ sig_inf,
+                                                            int32_t* __restrict__ sig_status) {
+  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 4;
+  const uint32_t ic = i < n ? i : n - 1;  // rows past the end decode the last signature again
+  int st = LB_OK;
+  g2a a;
+  bool inf = false;
+  if (sig_sizes != nullptr && sig_sizes[ic] != 96) {
+    st = LB_INVALID_SIZE;
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  } else {
+    uint32_t w[24];
+    const uint4* s = reinterpret_cast<const uint4*>(sigs + (size_t)96 * ic);
+    LB_UNROLL for (int k = 0; k < 6; k++) {
+      const uint4 v = s[k];
+      w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+    }
+    st = g2_decompress96_wp(w, a, inf, [](const fp& x, const uint32_t* e, int top) { return r1_pow_const(x, e, top); });
+  }
+  if (i >= n || (threadIdx.x & 15) != 0) return;
+  soa_st(sig_aff, n, i, a);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+  LB_UNROLL for (int k = 0; k < 12; k++) sig_aos[(size_t)12 * i + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  sig_inf[i] = inf ? 1u : 0u;
+  sig_status[i] = st;
+}
+#endif  // LB_KG
 // The same with 16 lanes per field element (4 per wave): the lanes of a row run the same item and
 // share its square roots' exponentiations as row products (lb_row.h r1_pow_const), for batches
 // with few distinct roots on a device running alone (latency: 1.5 -> ~0.6 ms per call).

@@ -36,6 +36,35 @@ LB_HD int g2_decompress96_w(const uint32_t* w, g2a& out, bool& inf) {
   out.y = y;
   return LB_OK;
 }
+// the same with the square root's exponentiations by pow (k_decompress_sigs_row: on a row)
+template <class Pow>
+LB_HD int g2_decompress96_wp(const uint32_t* w, g2a& out, bool& inf, Pow pow) {
+  inf = false;
+  const uint32_t f = w[0] & 0xffu;
+  if (!(f & 0x80)) return LB_BAD_ENCODING;
+  if (f & 0x40) {
+    uint32_t acc = w[0] & 0xffffff3fu;
+    for (int i = 1; i < 24; i++) acc |= w[i];
+    if (acc) return LB_BAD_ENCODING;
+    inf = true;
+    out.x = fp2_zero();
+    out.y = fp2_zero();
+    return LB_OK;
+  }
+  fp x1, x0;
+  const bool ok1 = fp_plain_from_be48_w(x1, w, 0x1f);
+  const bool ok0 = fp_plain_from_be48_w(x0, w + 12, 0xff);
+  if (!ok0 || !ok1) return LB_BAD_ENCODING;
+  const fp2 x{fp_to_mont(x0), fp_to_mont(x1)};
+  const fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), fp2_load(LB_B2));
+  fp2 y;
+  if (!fp2_sqrt_p(y, rhs, pow)) return LB_POINT_NOT_ON_CURVE;
+  const bool want_large = (f & 0x20) != 0;
+  if (fp2_lex_larger(y) != want_large) y = fp2_neg(y);
+  out.x = x;
+  out.y = y;
+  return LB_OK;
+}
 LB_HD int g2_decompress96(const uint8_t* b, g2a& out, bool& inf) {
   uint32_t w[24];
   LB_UNROLL for (int k = 0; k < 24; k++)

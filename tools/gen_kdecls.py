@@ -42,7 +42,7 @@ GROUPS = {
     10: ["k_miller_row", "k_tree_up_row"],
     11: ["k_ml_S_row", "k_root_check_row", "k_root_partial_row", "k_partials_check_row"],
     12: ["k_hash_finish_row"],
-    13: ["k_hash_map_row"],
+    13: ["k_hash_map_row", "k_decompress_sigs_row"],
 }
 N_GROUPS = len(GROUPS)
 GROUP_OF = {k: g for g, ks in GROUPS.items() for k in ks}
