@@ -792,6 +792,7 @@ enum {
   RK_MUL,    // dst = a b (Fp12)
   RK_SQR,    // dst = a^2
   RK_CSQR,   // dst = a^2, a cyclotomic
+  RK_CSQR2,  // dst = a^4, a cyclotomic (CSQR12X2)
   RK_FROB,   // dst = a^p
   RK_FROB2,  // dst = a^(p^2)
   RK_G2DBL,  // dst = 2a (6-slot Jacobian G2)
@@ -816,10 +817,18 @@ struct r_opl {
   // dst = a^|x| (a cyclotomic, dst != a)
   constexpr void pow_xabs(int dst, int a) {
     op(RK_COPY, dst, a, 12);
+    int run = 0;  // squarings pending (issued two at a time)
     for (int i = 62; i >= 0; i--) {
-      op(RK_CSQR, dst, dst);
-      if ((LB_X_ABS >> i) & 1ull) op(RK_MUL, dst, dst, a);
+      run++;
+      if ((LB_X_ABS >> i) & 1ull) {
+        for (; run >= 2; run -= 2) op(RK_CSQR2, dst, dst);
+        if (run) op(RK_CSQR, dst, dst);
+        run = 0;
+        op(RK_MUL, dst, dst, a);
+      }
     }
+    for (; run >= 2; run -= 2) op(RK_CSQR2, dst, dst);
+    if (run) op(RK_CSQR, dst, dst);
   }
   // dst = [|x|] a (G2, dst != a)
   constexpr void g2_mul_xabs(int dst, int a) {
@@ -926,6 +935,7 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
       case RK_MUL: prog = LBR_MUL12; na = 12; nb = 12; nout = 12; break;
       case RK_SQR: prog = LBR_SQR12; na = 12; nb = 0; nout = 12; break;
       case RK_CSQR: prog = LBR_CSQR12; na = 12; nb = 0; nout = 12; break;
+      case RK_CSQR2: prog = LBR_CSQR12X2; na = 12; nb = 0; nout = 12; break;
       case RK_FROB: prog = LBR_FROB; na = 12; nb = 0; nout = 12; break;
       case RK_FROB2: prog = LBR_FROB2; na = 12; nb = 0; nout = 12; break;
       case RK_G2DBL: prog = LBR_G2DBL; na = 6; nb = 0; nout = 6; break;

@@ -283,6 +283,12 @@ def build_programs():
         t = G.T(pg)
         pg.output(G.fp12_flat(cyclotomic_sqr(t, G.fp12_in(pg, 0))))
         progs["CSQR12"] = pg
+        # two chained cyclotomic squarings, the first's outputs never materialised (3 barriers
+        # instead of 2 x 2 plus a move out and back in)
+        pg = RowProg("CSQR12X2")
+        t = G.T(pg)
+        pg.output(G.fp12_flat(cyclotomic_sqr(t, cyclotomic_sqr(t, G.fp12_in(pg, 0)))))
+        progs["CSQR12X2"] = pg
         pg = RowProg("G2DBL")
         t = G.T(pg)
         pg.output(g2_flat(g2_dbl(t, g2_in(pg, 0))))
@@ -500,6 +506,8 @@ def _checks(codes):
         S.update({G.IN_BASE + k: to_row(flat[k]) for k in range(12)})
         got = [from_row(v) for v in run_row(codes["CSQR12"].words, S)]
         assert f12(got) == o.f12_sqr(g), "CSQR12"
+        got = [from_row(v) for v in run_row(codes["CSQR12X2"].words, S)]
+        assert f12(got) == o.f12_sqr(o.f12_sqr(g)), "CSQR12X2"
     # G2 point programs against the oracle's group law (affine results)
     def g2_row_in(Pa):
         (x0, x1), (y0, y1) = Pa
@@ -542,7 +550,7 @@ def _checks(codes):
         assert got == want, name
 
 
-ORDER = ["MUL12", "SQR12", "CSQR12", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2"]
+ORDER = ["MUL12", "SQR12", "CSQR12", "CSQR12X2", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2"]
 
 
 def const_limbs(v):
