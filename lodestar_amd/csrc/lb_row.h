@@ -796,6 +796,8 @@ enum {
   RK_FROB,   // dst = a^p
   RK_FROB2,  // dst = a^(p^2)
   RK_G2DBL,  // dst = 2a (6-slot Jacobian G2)
+  RK_G2DBL2, // dst = 4a
+  RK_G2DBL4, // dst = 16a
   RK_G2ADD,  // dst = a + b (no exceptional cases)
   RK_PSI,    // dst = psi(a)
   RK_PSI2,   // dst = psi^2(a)
@@ -831,12 +833,23 @@ struct r_opl {
     if (run) op(RK_CSQR, dst, dst);
   }
   // dst = [|x|] a (G2, dst != a)
+  constexpr void g2_dbls(int dst, int run) {
+    for (; run >= 4; run -= 4) op(RK_G2DBL4, dst, dst);
+    for (; run >= 2; run -= 2) op(RK_G2DBL2, dst, dst);
+    if (run) op(RK_G2DBL, dst, dst);
+  }
   constexpr void g2_mul_xabs(int dst, int a) {
     op(RK_COPY, dst, a, 6);
+    int run = 0;  // doublings pending (issued four / two at a time)
     for (int i = 62; i >= 0; i--) {
-      op(RK_G2DBL, dst, dst);
-      if ((LB_X_ABS >> i) & 1ull) op(RK_G2ADD, dst, dst, a);
+      run++;
+      if ((LB_X_ABS >> i) & 1ull) {
+        g2_dbls(dst, run);
+        run = 0;
+        op(RK_G2ADD, dst, dst, a);
+      }
     }
+    g2_dbls(dst, run);
   }
 };
 // r_final_exp after the inversion (Y0 = f^-1): the chain of lb_pairing.h final_exponentiation
@@ -939,6 +952,8 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
       case RK_FROB: prog = LBR_FROB; na = 12; nb = 0; nout = 12; break;
       case RK_FROB2: prog = LBR_FROB2; na = 12; nb = 0; nout = 12; break;
       case RK_G2DBL: prog = LBR_G2DBL; na = 6; nb = 0; nout = 6; break;
+      case RK_G2DBL2: prog = LBR_G2DBL2; na = 6; nb = 0; nout = 6; break;
+      case RK_G2DBL4: prog = LBR_G2DBL4; na = 6; nb = 0; nout = 6; break;
       case RK_G2ADD: prog = LBR_G2ADD; na = 6; nb = 6; nout = 6; break;
       case RK_PSI: prog = LBR_PSI; na = 6; nb = 0; nout = 6; break;
       case RK_PSI2: prog = LBR_PSI2; na = 6; nb = 0; nout = 6; break;

@@ -306,6 +306,14 @@ def build_programs():
         t = G.T(pg)
         pg.output(g2_flat(g2_psi2(t, pg, g2_in(pg, 0))))
         progs["PSI2"] = pg
+        for k in (2, 4):  # k chained doublings, intermediate points never materialised
+            pg = RowProg("G2DBL%d" % k)
+            t = G.T(pg)
+            P = g2_in(pg, 0)
+            for _ in range(k):
+                P = g2_dbl(t, P)
+            pg.output(g2_flat(P))
+            progs["G2DBL%d" % k] = pg
     finally:
         G.Prog = saved
     return progs
@@ -534,6 +542,10 @@ def _checks(codes):
         assert g2_row_out(got) == o.g2_psi(Pa), "PSI"
         got = [from_row(v) for v in run_row(codes["PSI2"].words, S)]
         assert g2_row_out(got) == o.g2_psi(o.g2_psi(Pa)), "PSI2"
+        got = [from_row(v) for v in run_row(codes["G2DBL4"].words, S)]
+        assert g2_row_out(got) == o.g2_mul(Pa, 16), "G2DBL4"
+        got = [from_row(v) for v in run_row(codes["G2DBL2"].words, S)]
+        assert g2_row_out(got) == o.g2_mul(Pa, 4), "G2DBL2"
     # a few Miller steps against the lone-lane programs' interpreter (values, not limbs)
     Pp = o.sk_to_pk(0x1234567)
     Qq = o.hash_to_g2(b"\x07" * 32)
@@ -550,7 +562,7 @@ def _checks(codes):
         assert got == want, name
 
 
-ORDER = ["MUL12", "SQR12", "CSQR12", "CSQR12X2", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2"]
+ORDER = ["MUL12", "SQR12", "CSQR12", "CSQR12X2", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2", "G2DBL2", "G2DBL4"]
 
 
 def const_limbs(v):
