@@ -667,7 +667,7 @@ def test_direct_verify_callers(engine):
         asyncio.run(pool.close())
 
 
-@pytest.mark.parametrize("name", ["c3_mixed", "c2"])
+@pytest.mark.parametrize("name", ["c3_mixed", "c2", "c3"])
 def test_per_root_kernel_forms_agree(monkeypatch, name):
     """The per-root chain has two forms per step, picked by the batch's distinct-root count: one
     lane per root (k_hash_finish, k_miller_lane) or 8 lanes per root (k_miller_g8, grouped LDS programs) and many
@@ -772,3 +772,42 @@ def test_row_engine_forms_agree(monkeypatch, name):
         assert np.array_equal(got, wl.expected), (row_fe, row_max, np.nonzero(got != wl.expected))
         outs.append(part)
     assert outs[0] == outs[1] == outs[2]
+
+
+@pytest.mark.gpu
+def test_headline_six_slot_batches_in_flight():
+    """The headline's own shape: 6-slot C3 batches (116 736 sets, 104 448 jobs, ~6 900 distinct
+    roots) as bench.py runs them, alone and with two engines in flight (so the under-load forms run:
+    one lane per root, lone-lane cofactor clearing, bucket MSM), and the same shape with one wrong
+    message per slot (the invalid-set search under load).  Per-job verdicts must equal the planted
+    expectation (valid: all 1; invalid: the reference's per-job re-verification, worker.ts:76-98)."""
+    import threading
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    with Engine(0) as e1, Engine(0) as e2:
+        wl = W.make(e1, "c3", slots=6)
+        wi = W.make(e1, "c3_invalid", slots=6)
+        assert wl.packed.n_sets == 116736 and (wl.expected == 1).all()
+        assert (wi.expected != 1).sum() >= 6
+        b1 = e1.upload(W.indexed_for(e1, wl))
+        b2 = e2.upload(W.indexed_for(e2, wi))
+        try:
+            assert np.array_equal(np.asarray(b1.verify()), wl.expected)
+            assert np.array_equal(np.asarray(b2.verify()), wi.expected)
+            res = {}
+
+            def run(k, b):
+                res[k] = [np.asarray(b.verify()).copy() for _ in range(3)]
+
+            ths = [threading.Thread(target=run, args=(1, b1)), threading.Thread(target=run, args=(2, b2))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            for r in res[1]:
+                assert np.array_equal(r, wl.expected)
+            for r in res[2]:
+                assert np.array_equal(r, wi.expected), np.nonzero(r != wi.expected)
+        finally:
+            b1.free()
+            b2.free()

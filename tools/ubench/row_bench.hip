@@ -96,6 +96,20 @@ __global__ void __launch_bounds__(LBR_NT) k_g2_ops(int iters, uint64_t* out) {
   const uint64_t t1 = rt();
   if (threadIdx.x == 0) out[0] = t1 - t0;
 }
+// dependent LDS load chain (latency of one ds_read round trip), NT threads each chasing
+template <int NT>
+__global__ void __launch_bounds__(NT) k_lds_chase(int iters, uint64_t* out, int* sink) {
+  __shared__ int A[4096];
+  for (int i = threadIdx.x; i < 4096; i += NT) A[i] = (i * 77 + 13) & 4095;
+  __syncthreads();
+  int p = threadIdx.x & 4095;
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) p = A[p];
+  __syncthreads();
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = p;
+}
 // synthetic one-phase programs written over the image at offset 0: the cost of a phase's parts
 template <int V>
 __global__ void __launch_bounds__(LBR_NT) k_synth(int iters, uint64_t* out) {
@@ -325,6 +339,8 @@ int main() {
       printf("\n");
     }
   }
+  run("lds chase (64 thr)", [&](int n) { hipLaunchKernelGGL(k_lds_chase<64>, dim3(1), dim3(64), 0, 0, n, d, sink); }, 10000);
+  run("lds chase (1024 thr)", [&](int n) { hipLaunchKernelGGL(k_lds_chase<1024>, dim3(1), dim3(1024), 0, 0, n, d, sink); }, 10000);
   run("synth P1 plain", [&](int n) { hipLaunchKernelGGL(k_synth<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth P1 8+8 terms", [&](int n) { hipLaunchKernelGGL(k_synth<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth P1 8+8 reduce", [&](int n) { hipLaunchKernelGGL(k_synth<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
