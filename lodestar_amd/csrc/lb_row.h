@@ -285,16 +285,28 @@ __device__ __forceinline__ void r_prefetch(const lds_i32* prog, int pos, int h0,
   if (t >= n) return;  // an idle row (its words are not used)
   const lds_i32* rec = prog + pos + t * rs;
   p.dst = rec[0];
-  LB_UNROLL for (int j = 0; j < 8; j++) p.w[j] = rec[1 + min(j, nA - 1)];
-  LB_UNROLL for (int j = 0; j < 8; j++) p.w[8 + j] = rec[nB > 0 ? offB + min(j, nB - 1) : 1];
+  // in blocks of 4 terms: the second block only when the phase's operands have more than 4
+  // (nA, nB are phase-uniform: scalar branches)
+  LB_UNROLL for (int j = 0; j < 4; j++) p.w[j] = rec[1 + min(j, nA - 1)];
+  if (nA > 4) LB_UNROLL for (int j = 4; j < 8; j++) p.w[j] = rec[1 + min(j, nA - 1)];
+  LB_UNROLL for (int j = 0; j < 4; j++) p.w[8 + j] = rec[nB > 0 ? offB + min(j, nB - 1) : 1];
+  if (nB > 4) LB_UNROLL for (int j = 4; j < 8; j++) p.w[8 + j] = rec[offB + min(j, nB - 1)];
 }
-// sum of up to 8 prefetched terms w[O .. O + 8) (n of them; the rest coefficient 0)
+// sum of the 4 prefetched terms w[O .. O + 4) (tools/gen_row_programs.py pads every non-plain
+// operand and linear task to whole blocks of 4 with zero-coefficient pairs: no mask)
+template <int O>
+__device__ __forceinline__ int64_t r_acc4(const lds_i32* S, const r_pref& p, int, int k) {
+  int v[4];
+  LB_UNROLL for (int j = 0; j < 4; j++) v[j] = S[16 * (p.w[O + j] & 0xffff) + k];
+  int64_t acc = 0;
+  LB_UNROLL for (int j = 0; j < 4; j++) acc += (int64_t)(p.w[O + j] >> 16) * v[j];
+  return acc;
+}
+// sum of up to 8 prefetched terms w[O .. O + 8) (n of them)
 template <int O>
 __device__ __forceinline__ int64_t r_acc_w(const lds_i32* S, const r_pref& p, int n, int k) {
-  int v[8];
-  LB_UNROLL for (int j = 0; j < 8; j++) v[j] = S[16 * (p.w[O + j] & 0xffff) + k];
-  int64_t acc = 0;
-  LB_UNROLL for (int j = 0; j < 8; j++) acc += (int64_t)(j < n ? (p.w[O + j] >> 16) : 0) * v[j];
+  int64_t acc = r_acc4<O>(S, p, n, k);
+  if (n > 4) acc += r_acc4<O + 4>(S, p, n - 4, k);
   return acc;
 }
 template <int O>
@@ -340,7 +352,11 @@ __device__ void r_exec_tail(lds_i32* S, const lds_i32* prog, int pos, int h0, in
 // Run one program (offset `off` in the image): inputs already in IN, outputs left in the temps
 // the header lists.  r_exec_inl is inlined once into r_run's loop (lb_row.h, end): a call of the
 // out-of-line r_exec costs ~0.9 us of callee-saved scratch round trips, on the order of a phase.
+#ifndef LBR_TL
+#define LBR_TL(i)
+#endif
 __device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) {
+  LBR_TL(0);
   lds_i32* S = r_lds(S_generic);
   const lds_i32* prog = r_progs(S_generic) + off;
   const int k = r_limb(), row = r_row(), pk = r_plimb(k);
@@ -350,6 +366,7 @@ __device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) {
   pos += 2;
   r_pref p;
   r_prefetch(prog, pos, h0, h1, row, p);
+  LBR_TL(1);
   for (int ph = 0; ph < nph; ph++) {
     const int kind = h0 & 0xff, flags = (h0 >> 8) & 0xff, n = h0 >> 16;
     const int nx = h1 & 0xffff, ny = h1 >> 16;
@@ -381,12 +398,14 @@ __device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) {
         yv = r_reduce(acc, k, pk);
       }
     }
+    LBR_TL(2);
     int nh0 = 0, nh1 = 0;
     if (more) {
       nh0 = __builtin_amdgcn_readfirstlane(nh0v);
       nh1 = __builtin_amdgcn_readfirstlane(nh1v);
       r_prefetch(prog, npos + 2, nh0, nh1, row, p);
     }
+    LBR_TL(3);
     if (act) {
       if (kind == 0) {
         int x[14];
@@ -395,8 +414,10 @@ __device__ __forceinline__ void r_exec_inl(int32_t* S_generic, int off) {
       }
       S[16 * dst + k] = yv;
     }
+    LBR_TL(4);
     if (n > LBR_NROWS) r_exec_tail(S, prog, pos, h0, h1);
     if (kind != 0 || !(flags & 16)) r_sync();  // flag 16: the next (linear) phase reads nothing of this one
+    LBR_TL(5);
 #ifdef LBR_PHASE_HOOK
     LBR_PHASE_HOOK(ph, kind, n);
 #endif

@@ -382,6 +382,9 @@ def encode(pg):
             phases.append((1, [l for l in pg.lins if l[0] == s and l[1] == v and id(l) not in moved], 0))
     out = [len(phases), len(pg.outs)] + list(pg.outs)
 
+    def pad4(n):
+        return (n + 3) // 4 * 4
+
     def pairs(lin, width):
         ps = [_pair(s, c) for s, c in sorted(lin.d.items())]
         assert len(ps) <= width
@@ -399,6 +402,10 @@ def encode(pg):
         if kind == 0:
             xs, ys = [t[2] for t in tasks], [t[3] for t in tasks]
             nx, ny = max(len(x.d) for x in xs), max(len(y.d) for y in ys)
+            # operand sums are read in blocks of 4 terms (lb_row.h r_acc4): pad to whole blocks
+            # with zero-coefficient pairs, so the interpreter needs no per-term mask
+            nx = nx if plain(xs) else pad4(nx)
+            ny = ny if plain(ys) else pad4(ny)
             flags = (1 if plain(xs) else 0) | (2 if plain(ys) else 0)
             flags |= (4 if reduce(xs) else 0) | (8 if reduce(ys) else 0)
             flags |= 16 if arg else 0
@@ -407,7 +414,7 @@ def encode(pg):
                 out += [t[1]] + pairs(t[2], nx) + pairs(t[3], ny)
         else:
             ls = [t[3] for t in tasks]
-            nx = max(len(l.d) for l in ls)
+            nx = pad4(max(len(l.d) for l in ls))
             out += [kind | (len(tasks) << 16), nx | (arg << 16)]
             for t in tasks:
                 out += [t[2]] + pairs(t[3], nx)

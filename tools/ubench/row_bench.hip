@@ -26,6 +26,19 @@ __device__ int g_ph_n;
     g_ph_n++;                                                                        \
   }
 #endif
+#ifdef UB_TL
+// a timeline of r_exec_inl (lb_row.h LBR_TL points): thread 0 of each wave adds the s_memtime
+// delta since the previous point to its wave's LDS slot (no global memory inside the loop)
+static __shared__ unsigned long long g_tl[16][8];
+static __shared__ unsigned long long g_tl_prev[16];
+#define LBR_TL(i)                                                    \
+  if ((threadIdx.x & 63) == 0) {                                    \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();    \
+    g_tl[threadIdx.x >> 6][i] += now - g_tl_prev[threadIdx.x >> 6]; \
+    g_tl_prev[threadIdx.x >> 6] = now;                              \
+  }
+__device__ unsigned long long g_tl_out[16][8];
+#endif
 #include "lb_kernels.h"
 
 __device__ __forceinline__ uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
@@ -150,6 +163,24 @@ __global__ void __launch_bounds__(LBR_NT) k_synth(int iters, uint64_t* out) {
   const uint64_t t1 = rt();
   if (threadIdx.x == 0) out[0] = t1 - t0;
 }
+#ifdef UB_TL
+// timeline of r_exec_inl over `iters` runs of program `prog` (image staged in full)
+__global__ void __launch_bounds__(LBR_NT) k_tl(int iters, int prog, int g2) {
+  LBR_SHARED_N(S, LBR_PROGS_END);
+  r_init(S, LBR_PROGS_END, 0);
+  ub_fill_ones(S, LBR_A(0), 12);
+  r_copy(S, LBR_IN, LBR_A(0), 24);
+  if ((threadIdx.x & 63) == 0) {
+    for (int i = 0; i < 8; i++) g_tl[threadIdx.x >> 6][i] = 0;
+    g_tl_prev[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+  }
+  r_sync();
+  for (int it = 0; it < iters; it++) r_exec_inl(S, prog);
+  r_sync();
+  if ((threadIdx.x & 63) == 0)
+    for (int i = 0; i < 8; i++) g_tl_out[threadIdx.x >> 6][i] = g_tl[threadIdx.x >> 6][i];
+}
+#endif
 template <int OP>
 __global__ void __launch_bounds__(LBR_NT) k_phases(unsigned long long* out) {
   LBR_SHARED_N(S, LBR_PROGS_END);
@@ -349,6 +380,24 @@ int main() {
   run("synth P16 plain", [&](int n) { hipLaunchKernelGGL(k_synth<6>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth P64 plain", [&](int n) { hipLaunchKernelGGL(k_synth<8>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth barrier", [&](int n) { hipLaunchKernelGGL(k_synth<7>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
+#ifdef UB_TL
+  {
+    const int progs[4] = {LBR_G2DBL, LBR_CSQR12, LBR_MUL12, LBR_G2ADD};
+    const char* names[4] = {"G2DBL", "CSQR12", "MUL12", "G2ADD"};
+    for (int q = 0; q < 4; q++) {
+      hipLaunchKernelGGL(k_tl, dim3(1), dim3(LBR_NT), 0, 0, 100, progs[q], 0);
+      hipDeviceSynchronize();
+      unsigned long long tl[16][8];
+      hipMemcpyFromSymbol(tl, HIP_SYMBOL(g_tl_out), sizeof(tl));
+      printf("timeline %s (s_memtime ticks per exec, waves 0..3): entry->prologue, operands, next-prefetch, product+store, barrier, loop-back\n", names[q]);
+      for (int w = 0; w < 4; w++) {
+        printf("  wave %d:", w);
+        for (int i = 0; i < 6; i++) printf(" %8.1f", tl[w][(i + 1) % 6] / 100.0);
+        printf("\n");
+      }
+    }
+  }
+#endif
   run("row G2 dbl", [&](int n) { hipLaunchKernelGGL(k_g2_ops<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row G2 add", [&](int n) { hipLaunchKernelGGL(k_g2_ops<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
   run("row G2DBL exec only", [&](int n) { hipLaunchKernelGGL(k_g2_ops<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 200);
