@@ -68,11 +68,20 @@ int32_t lb_abi_version(void);
  * One engine = one batch in flight on one GPU (own HIP streams and device workspaces); a process
  * may drive several engines per GPU concurrently (the reference runs one job package per worker
  * thread at a time, multithread/index.ts:290-381).  device < 0 = current.  Returns
- * LB_ERR_DEVICE once the per-device engine cap is reached (7, or LB_MAX_ENGINES_PER_DEVICE):
- * past it, a dispatch of the per-root kernels can fail to get private-segment scratch and the HSA
- * queue aborts asynchronously (measured at 8 engines, profiles/r2_inflight8_abort.txt).
+ * LB_ERR_DEVICE once the per-device engine cap is reached (10, or LB_MAX_ENGINES_PER_DEVICE;
+ * each engine's scratch for the largest private segment is reserved at creation, so an exhausted
+ * pool fails here instead of aborting a queue later).
  */
 int32_t lb_engine_create(int32_t device, lb_engine** out);
+/*
+ * The same with flags.  LB_ENGINE_LATENCY: the engine is the device's latency engine (the
+ * reference's verifyOnMainThread path, multithread/index.ts:138-151): its streams run on a
+ * reserved set of CUs (LB_LATENCY_CUS, default 8) and it always takes the small-batch latency
+ * forms; engines created AFTER it on the device run on the remaining CUs, so a 1-set call does not
+ * queue behind the pool's batches.  Create the latency engine first.
+ */
+#define LB_ENGINE_LATENCY 1u
+int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out);
 void lb_engine_destroy(lb_engine* e);
 
 /*

@@ -6,6 +6,7 @@
 // (the reference structured-clones its BlsWorkReq[], multithread/index.ts:330), so the
 // caller never has to keep its buffers alive.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -108,6 +109,9 @@ struct lb_batch {
 #endif
 struct lb_engine {
   int device = 0;
+  // LB_ENGINE_LATENCY (lb_engine_create_ex): streams confined to the device's reserved CUs, the
+  // latency forms always (the partition keeps every other engine off those CUs)
+  bool latency = false;
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
   hipStream_t stream3 = nullptr;  // s3: pubkey aggregation + blinding, beside the signature decode
@@ -252,11 +256,18 @@ static exit_rec g_device_exit[64][2];
 static int64_t lb_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// CUs reserved for latency engines per device (0: no partition yet); engines created while a
+// partition exists run on the complement.  LB_LATENCY_CUS (default 8 of the device's CUs).
+static int g_latency_cus[64];
 struct busy_scope {
   int dev;
   const void* eng;
-  busy_scope(int d, const void* e) : dev(d), eng(e) { g_device_busy[dev].fetch_add(1, std::memory_order_relaxed); }
+  bool counted;
+  busy_scope(int d, const void* e, bool latency = false) : dev(d), eng(e), counted(!latency) {
+    if (counted) g_device_busy[dev].fetch_add(1, std::memory_order_relaxed);
+  }
   ~busy_scope() {
+    if (!counted) return;  // a latency engine's calls run on its own CUs: not load for the others
     {
       std::lock_guard<std::mutex> lk(g_exit_mu[dev]);
       exit_rec* r = g_device_exit[dev];
@@ -275,6 +286,7 @@ struct busy_scope {
 #endif
 template <class E>
 static bool device_alone(const E* e) {
+  if (e->latency) return true;  // its reserved CUs run nothing else
   if (g_device_busy[e->device].load(std::memory_order_relaxed) > 1) return false;
   int64_t other;
   {
@@ -352,8 +364,15 @@ const char* lb_error_name(int32_t code) {
   }
 }
 
-int32_t lb_engine_create(int32_t device, lb_engine** out) {
-  if (!out) return LB_ERR_ARGUMENT;
+int32_t lb_engine_create(int32_t device, lb_engine** out) { return lb_engine_create_ex(device, 0u, out); }
+// a CU mask over [lo, hi) of ncu CUs (32 per word)
+static std::vector<uint32_t> cu_mask(int ncu, int lo, int hi) {
+  std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
+  for (int c = lo; c < hi && c < ncu; c++) m[(size_t)c / 32] |= 1u << (c % 32);
+  return m;
+}
+int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
+  if (!out || (flags & ~LB_ENGINE_LATENCY)) return LB_ERR_ARGUMENT;
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return LB_ERR_NO_DEVICE;
@@ -413,9 +432,33 @@ int32_t lb_engine_create(int32_t device, lb_engine** out) {
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SPEC_GSUM")) e->spec_gsum = std::atoi(sm) != 0;
-  if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, prio_least) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking) != hipSuccess ||
+  // CU partition: a latency engine's streams on the reserved CUs [0, R), every engine created
+  // while a partition exists on [R, ncu)
+  bool masked = false;
+  std::vector<uint32_t> mask;
+  {
+    std::lock_guard<std::mutex> lk(g_engine_mu);
+    const int ncu = prop.multiProcessorCount;
+    if (flags & LB_ENGINE_LATENCY) {
+      if (g_latency_cus[device] == 0) {
+        const char* v = getenv("LB_LATENCY_CUS");
+        const int r = v ? atoi(v) : 8;
+        g_latency_cus[device] = std::max(1, std::min(r, ncu / 4));
+      }
+      e->latency = true;
+      mask = cu_mask(ncu, 0, g_latency_cus[device]);
+      masked = true;
+    } else if (g_latency_cus[device] > 0) {
+      mask = cu_mask(ncu, g_latency_cus[device], ncu);
+      masked = true;
+    }
+  }
+  auto mk = [&](hipStream_t* st, bool prio) {
+    if (masked) return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+    return prio ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio_least)
+                : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  };
+  if (mk(&e->stream, true) != hipSuccess || mk(&e->stream2, false) != hipSuccess || mk(&e->stream3, false) != hipSuccess ||
       hipHostMalloc((void**)&e->h_nu, 8, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_flag, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
@@ -1703,7 +1746,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   const uint32_t nj = b->n_jobs;
   if (nj == 0) return LB_OK;
   uint32_t m = 1, mu = 1;
-  busy_scope busy(e->device, e);
+  busy_scope busy(e->device, e, e->latency);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   // root verdict on s1 (after the join)
@@ -1750,7 +1793,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
     fp12_to_be576(out576, fp12_one());
     return LB_OK;
   }
-  busy_scope busy(e->device, e);
+  busy_scope busy(e->device, e, e->latency);
   int32_t st = run_pipeline(e, b, scalars, m, mu);
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
@@ -1778,7 +1821,7 @@ extern "C" int32_t lb_batch_search_after_partial(lb_engine* e, lb_batch* b, int3
   if (b->n_jobs == 0) return LB_OK;
   if (e->partial_serial == 0 || e->partial_serial != b->serial) return LB_ERR_ARGUMENT;  // another call ran since
   LB_HIP(hipSetDevice(e->device));
-  busy_scope busy(e->device, e);
+  busy_scope busy(e->device, e, e->latency);
   const uint32_t mu = e->partial_mu, nj = b->n_jobs;
   LB_HIP(e->verdict.ensure(4));
   LB_HIP(e->y_root.ensure(576));

@@ -170,10 +170,12 @@ class Batch:
 class Engine:
     """One lb_engine bound to one gfx950 device."""
 
-    def __init__(self, device: int = 0):
+    LATENCY = 1  # lb_engine_create_ex flag LB_ENGINE_LATENCY (include/lodestar_bls.h)
+
+    def __init__(self, device: int = 0, flags: int = 0):
         self.lib = N.load()
         h = ctypes.c_void_p()
-        _check(self.lib.lb_engine_create(int(device), ctypes.byref(h)))
+        _check(self.lib.lb_engine_create_ex(int(device), ctypes.c_uint32(flags), ctypes.byref(h)))
         self.h = h
         self.device = device
 

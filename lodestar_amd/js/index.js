@@ -199,7 +199,7 @@ function codeToResult(code) {
 
 class BlsGpuVerifier {
   /**
-   * @param {{device?: number, engines?: number, blsVerifyAllMultiThread?: boolean}} [opts]
+   * @param {{device?: number, engines?: number, blsVerifyAllMultiThread?: boolean, latencyPartition?: boolean}} [opts]
    * @param {{logger?: object, metrics?: object|null}} [modules] as the reference pool's
    *   (multithread/index.ts:98-134): `metrics.blsThreadPool.*` / `metrics.bls.*` receive the same
    *   updates (lodestar.ts:433-523) when given
@@ -212,11 +212,19 @@ class BlsGpuVerifier {
     const device = opts.device === undefined ? 0 : opts.device;
     this.engines = [];
     try {
+      // synchronous calls get their own engine, created first as the device's latency engine
+      // (LB_ENGINE_LATENCY: its own reserved CUs, the pool's engines on the rest), so a
+      // verifyOnMainThread call is neither queued behind a pool batch's engine mutex nor behind
+      // the pool's kernels on the device
+      try {
+        this.syncEngine = addon.createEngine(device, opts.latencyPartition === false ? 0 : 1);
+      } catch (e) {
+        this.syncEngine = addon.createEngine(device);
+      }
       for (let k = 0; k < n; k++) this.engines.push(addon.createEngine(device));
-      // synchronous calls get their own engine: never queued behind a pool batch's engine mutex
-      this.syncEngine = addon.createEngine(device);
     } catch (e) {
       for (const en of this.engines) addon.destroyEngine(en);
+      if (this.syncEngine) addon.destroyEngine(this.syncEngine);
       throw e;
     }
     this.idle = this.engines.slice();

@@ -17,7 +17,7 @@
  *   - argument lengths are checked against the offsets before anything is queued (TypeError).
  *
  * Exports:
- *   createEngine(device: number) -> External
+ *   createEngine(device: number, flags?: number) -> External   (flags: 1 = LB_ENGINE_LATENCY)
  *       (the first call raises GPU_MAX_HW_QUEUES to 16 when it is unset or lower -- HIP's and the
  *       GPU boxes' default is 4 -- so the three HIP streams of each engine get their own hardware
  *       queue)
@@ -126,11 +126,13 @@ static napi_value throw_code(napi_env env, int32_t code) {
 
 static napi_value create_engine(napi_env env, napi_callback_info info) {
   static int queues_set = 0;
-  size_t argc = 1;
-  napi_value argv[1];
+  size_t argc = 2;
+  napi_value argv[2];
   int32_t device = 0;
+  uint32_t flags = 0;
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   if (argc >= 1) NAPI_CALL(env, napi_get_value_int32(env, argv[0], &device));
+  if (argc >= 2) NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &flags));
   if (!queues_set) {
     /* HIP reads GPU_MAX_HW_QUEUES once, at runtime initialisation (the first engine): each
      * engine drives three streams, and with the default 4 queues the streams of concurrent
@@ -141,7 +143,7 @@ static napi_value create_engine(napi_env env, napi_callback_info info) {
     queues_set = 1;
   }
   engine_box* b = (engine_box*)calloc(1, sizeof(engine_box));
-  int32_t st = lb_engine_create(device, &b->e);
+  int32_t st = lb_engine_create_ex(device, flags, &b->e);
   if (st != LB_OK) {
     free(b);
     return throw_code(env, st);

@@ -4,6 +4,7 @@ batches use size-independent properties (all-valid accepts; exactly the planted 
 jobs are rejected; partial products over shards agree)."""
 import asyncio
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -811,3 +812,22 @@ def test_headline_six_slot_batches_in_flight():
         finally:
             b1.free()
             b2.free()
+
+
+@pytest.mark.gpu
+def test_latency_engine_under_load():
+    """LB_ENGINE_LATENCY (lb_engine_create_ex): the latency engine, created first, runs on its
+    reserved CUs with the latency forms while two engines created after it (the complement of the
+    CUs) verify 6-slot C3 batches; every verdict must match, and the 1-set calls must not queue
+    behind the pool.  In a child process with GPU_MAX_HW_QUEUES=16, as the drop-in sets it (HIP
+    reads it once per process; with the default 4 queues the engines' streams share hardware
+    queues and a 1-set call waits behind a pool kernel on its queue)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gpu_latency_child.py")],
+                       env=env, capture_output=True, text=True, timeout=240)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    ms = [float(x) for x in r.stdout.strip().splitlines()[-1].split()]
+    assert sorted(ms)[len(ms) // 2] < 8.0, ms
