@@ -430,6 +430,7 @@ def latency_leg(eng, W, wc1):
     ip2 = W.indexed_for(eng, wc2)
     assert eng.verify_jobs_packed(ip2) == list(wc2.expected)
     out["latency_block_ms"] = median_ms(lambda: eng.verify_jobs_packed(ip2), 10)
+    out["latency_block_stage_ms"] = profiled_stages(eng, lambda: eng.verify_jobs_packed(ip2))
     return out
 
 

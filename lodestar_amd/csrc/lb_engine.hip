@@ -1057,17 +1057,22 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_sig_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
                            e->s_terms.as<uint32_t>());
-      // 64:1 levels, ping-ponging between the two buffers; the last level writes treeS[1]
-      uint32_t* bufs[2] = {e->s_terms.as<uint32_t>(), e->s_part.as<uint32_t>()};
-      uint32_t m = n;
-      int cur = 0;
-      while (m > 64) {
-        const uint32_t mo = (m + 63) / 64;
-        hipLaunchKernelGGL(k_g2_sum64, dim3(mo), dim3(64), 0, s2, m, bufs[cur], mo, bufs[cur ^ 1], 0u);
-        m = mo;
-        cur ^= 1;
+      if (n <= e->small_s_g8_max) {  // one workgroup of 8-lane additions
+        hipLaunchKernelGGL(k_g2_sum_g8, dim3(1), dim3(8 * LB_SUM_G8_GROUPS), 0, s2, n, e->s_terms.as<uint32_t>(),
+                           2 * mj, e->treeS.as<uint32_t>(), 1u);
+      } else {
+        // 64:1 levels, ping-ponging between the two buffers; the last level writes treeS[1]
+        uint32_t* bufs[2] = {e->s_terms.as<uint32_t>(), e->s_part.as<uint32_t>()};
+        uint32_t m = n;
+        int cur = 0;
+        while (m > 64) {
+          const uint32_t mo = (m + 63) / 64;
+          hipLaunchKernelGGL(k_g2_sum64, dim3(mo), dim3(64), 0, s2, m, bufs[cur], mo, bufs[cur ^ 1], 0u);
+          m = mo;
+          cur ^= 1;
+        }
+        hipLaunchKernelGGL(k_g2_sum64, dim3(1), dim3(64), 0, s2, m, bufs[cur], 2 * mj, e->treeS.as<uint32_t>(), 1u);
       }
-      hipLaunchKernelGGL(k_g2_sum64, dim3(1), dim3(64), 0, s2, m, bufs[cur], 2 * mj, e->treeS.as<uint32_t>(), 1u);
     } else {
       stage_scope sc(e, ST_SIG_MSM, s2);
       LB_HIP(hipMemsetAsync(e->bcnt.p, 0, (size_t)LB_MSM_NB * 4, s2));

@@ -1690,6 +1690,40 @@ __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* 
 }
 #endif  // LB_KG
 
+// The same sum for small n in ONE workgroup with 8-lane G2 additions (lb_group.h g8_add: 6
+// product levels instead of 43 serial products per addition): 64 groups each add a strided share,
+// then a 6-level tree over the groups through LDS.  For the small-S path up to small_s_g8_max
+// terms (a block: ~0.6 ms of lone-lane 64:1 trees -> ~0.1 ms).
+#define LB_SUM_G8_GROUPS 64
+#if LB_KG(9)
+__global__ void __launch_bounds__(8 * LB_SUM_G8_GROUPS) k_g2_sum_g8(uint32_t n, const uint32_t* __restrict__ in,
+                                                                  uint32_t n_out, uint32_t* __restrict__ out,
+                                                                  uint32_t out0) {
+  __shared__ uint32_t st[LB_SUM_G8_GROUPS * 72];
+  const int g = threadIdx.x >> 3, q = g8_q();
+  g2j acc = jac_infinity<fp2>();
+  for (uint32_t i = g; i < n; i += LB_SUM_G8_GROUPS) g8_add(acc, soa_ld<g2j>(in, n, i));
+  auto stash = [&](int slot, const g2j& v) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+    LB_UNROLL for (int k = 0; k < 9; k++) st[slot * 72 + 8 * k + q] = w[8 * k + q];
+  };
+  stash(g, acc);
+  __syncthreads();
+  for (int s = LB_SUM_G8_GROUPS / 2; s >= 1; s >>= 1) {
+    if (g < s) {
+      g2j o;
+      uint32_t* w = reinterpret_cast<uint32_t*>(&o);
+      LB_UNROLL for (int k = 0; k < 72; k++) w[k] = st[(g + s) * 72 + k];
+      g8_add(acc, o);
+    }
+    __syncthreads();
+    if (g < s) stash(g, acc);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) soa_st(out, n_out, out0, acc);
+}
+#endif  // LB_KG
+
 // ---------------------------------------------------------------- invalid-set search
 // After a failing root check the engine searches for the failing sets over NODES: a node is a
 // contiguous range [lo_j, lo_j + len_j) of the members array (sets sorted by signing root) and

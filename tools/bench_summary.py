@@ -12,7 +12,7 @@ for k in ("value_distinct_keys", "distinct_keys", "value_one_invalid_per_batch",
           "latency_block_ms", "value_dropin", "batch_latency_ms", "dropin", "signing_roots"):
     if k in d:
         print(k, d[k])
-for k in ("slots1_stage_ms", "latency_1set_stage_ms"):
+for k in ("slots1_stage_ms", "latency_1set_stage_ms", "latency_block_stage_ms"):
     if k in d:
         print(k, d[k])
 if "invalid_batch_stage_ms" in d:

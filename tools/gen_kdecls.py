@@ -38,7 +38,7 @@ GROUPS = {
         "k_rsm_terms", "k_smsm_terms_pre", "k_range_pk", "k_test_pk", "k_g1_terms", "k_g1_sum64", "k_g1_out48",
         "k_kzg_setup_g1", "k_kzg_setup_g2"],
     8: ["k_hash_finish_g8"],
-    9: ["k_msm_buckets_g8", "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind_g8", "k_sig_blind", "k_g2_sum64", "k_sig_unblinded"],
+    9: ["k_msm_buckets_g8", "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind_g8", "k_sig_blind", "k_g2_sum64", "k_sig_unblinded", "k_g2_sum_g8"],
     10: ["k_miller_row", "k_tree_up_row"],
     11: ["k_ml_S_row", "k_root_check_row", "k_root_partial_row", "k_partials_check_row"],
     12: ["k_hash_finish_row"],
