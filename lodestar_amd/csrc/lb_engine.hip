@@ -1049,7 +1049,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       stage_scope sc(e, ST_SIG_MSM, s2);
       LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
       LB_HIP(e->s_part.ensure((size_t)((n + 63) / 64) * sizeof(g2j)));
-      if (n <= e->small_s_g8_max)
+      if (n <= e->row_max && e->alone && e->row_fe)
+        hipLaunchKernelGGL(k_sig_blind_row, dim3(n), dim3(LBR_NT), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
+                           e->s_terms.as<uint32_t>());
+      else if (n <= e->small_s_g8_max)
         hipLaunchKernelGGL(k_sig_blind_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
                            e->s_terms.as<uint32_t>());

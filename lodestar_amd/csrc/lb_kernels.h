@@ -1694,6 +1694,64 @@ __global__ void __launch_bounds__(64) k_g2_sum64(uint32_t n_in, const uint32_t* 
 // product levels instead of 43 serial products per addition): 64 groups each add a strided share,
 // then a 6-level tree over the groups through LDS.  For the small-S path up to small_s_g8_max
 // terms (a block: ~0.6 ms of lone-lane 64:1 trees -> ~0.1 ms).
+// r_i sig_i for small batches on the row engine (one workgroup per set; lb_row.h G2 programs):
+// the GLV double-and-add of k_sig_blind_g8 over the table t1 = sig, t2 = [lambda] sig =
+// -psi^2(sig), t3 = t1 + t2, starting from the top non-zero digit (no infinity in the ladder), the
+// additions with the exceptional-case tests (r_g2_add).  Jacobian result, canonical words.
+#if LB_KG(12)
+__global__ void __launch_bounds__(LBR_NT) k_sig_blind_row(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                        const uint64_t* __restrict__ scalars,
+                                                        const uint32_t* __restrict__ set_live,
+                                                        const uint32_t* __restrict__ sig_inf,
+                                                        uint32_t* __restrict__ terms) {
+  LBR_SHARED_N(S, LBR_PROGS_END - LBR_G2DBL);
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  if (!msm_live(i, set_live, sig_inf)) {  // uniform
+    if (threadIdx.x == 0) soa_st(terms, n, i, jac_infinity<fp2>());
+    return;
+  }
+  r_init(S, LBR_PROGS_END - LBR_G2DBL, LBR_G2DBL);
+  const int T1 = LBR_A(0), T2 = LBR_A(0) + 6, T3 = LBR_A(1), ACC = LBR_A(1) + 6;
+  {
+    const int t = r_tid();
+    if (t < 6) {  // x.c0 x.c1 y.c0 y.c1 from the affine SoA, z = 1
+      fp v;
+      if (t < 4)
+        LB_UNROLL for (int w = 0; w < 12; w++) v.v[w] = sig_aff[(size_t)(12 * t + w) * n + i];
+      else
+        v = t == 4 ? fp_one() : fp_zero();
+      r_stage_fp(S, t, v);
+    }
+    r_sync();
+    r_import_staged(S, T1, 6);
+  }
+  r_g2_psi2(S, T2, T1);
+  r_g2_neg(S, T2);  // [lambda] sig = -psi^2(sig)
+  r_g2_add(S, T3, T1, T2);
+  const uint64_t w = scalars[i];
+  const uint32_t k0 = (uint32_t)w, k1 = (uint32_t)(w >> 32);
+  auto digit = [&](int b) { return ((k0 >> b) & 1u) | (((k1 >> b) & 1u) << 1); };
+  int b = 31;
+  while (b >= 0 && digit(b) == 0) b--;
+  if (b < 0) {  // r = 0 (never for the engine's scalars): the identity
+    if (threadIdx.x == 0) soa_st(terms, n, i, jac_infinity<fp2>());
+    return;
+  }
+  auto tab = [&](uint32_t d) { return d == 1 ? T1 : (d == 2 ? T2 : T3); };
+  r_copy(S, ACC, tab(digit(b)), 6);
+  for (b--; b >= 0; b--) {
+    r_g2_dbl(S, ACC, ACC);
+    const uint32_t d = digit(b);
+    if (d) r_g2_add(S, ACC, ACC, tab(d));
+  }
+  r_export(S, ACC, 6);
+  if (threadIdx.x < 6) {
+    const fp v = r_fp_of_staged(S, threadIdx.x);
+    LB_UNROLL for (int k = 0; k < 12; k++) terms[(size_t)(12 * threadIdx.x + k) * n + i] = v.v[k];
+  }
+}
+#endif  // LB_KG
 #define LB_SUM_G8_GROUPS 64
 #if LB_KG(9)
 __global__ void __launch_bounds__(8 * LB_SUM_G8_GROUPS) k_g2_sum_g8(uint32_t n, const uint32_t* __restrict__ in,
