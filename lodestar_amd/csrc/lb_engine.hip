@@ -965,7 +965,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                            e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
       // (8 lanes per signature also for a slot while the device is otherwise idle ran slower:
       // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
-      if (n <= e->subgroup_g8_max)
+      if (n <= e->row_max && e->alone && e->row_fe)
+        hipLaunchKernelGGL(k_sig_subgroup_row, dim3(n), dim3(LBR_NT), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      else if (n <= e->subgroup_g8_max)
         hipLaunchKernelGGL(k_sig_subgroup_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
       else

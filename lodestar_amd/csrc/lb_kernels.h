@@ -327,6 +327,52 @@ __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32
 }
 #endif  // LB_KG
 
+// The same check on the row engine for small batches while alone (one workgroup per signature):
+// [|x|]P by the op list's fast ladder (a zero Z, the mark of any exceptional case, reruns it with
+// the tested additions: inputs here are adversarial), psi(P) by one program, the comparison on
+// thread 0 (jac_eq on the exported canonical words).
+#if LB_KG(12)
+__global__ void __launch_bounds__(LBR_NT) k_sig_subgroup_row(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                           const uint32_t* __restrict__ sig_inf,
+                                                           int32_t* __restrict__ sig_status) {
+  LBR_SHARED_N(S, LBR_PROGS_END - LBR_G2DBL);
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  if (sig_status[i] != LB_OK || sig_inf[i]) return;  // uniform
+  r_init(S, LBR_PROGS_END - LBR_G2DBL, LBR_G2DBL);
+  const int P = LBR_A(3), X = LBR_A(4), PSI = LBR_A(4) + 6;
+  {
+    const int t = r_tid();
+    if (t < 6) {
+      fp v;
+      if (t < 4)
+        LB_UNROLL for (int w = 0; w < 12; w++) v.v[w] = sig_aff[(size_t)(12 * t + w) * n + i];
+      else
+        v = t == 4 ? fp_one() : fp_zero();
+      r_stage_fp(S, t, v);
+    }
+    r_sync();
+    r_import_staged(S, P, 6);
+  }
+  r_run(S, &LBR_OPS_XLADDER, LBR_OPS_XLADDER.n);
+  if (r_zero_mask(S, 2, [&](int e) { return X + 4 + e; }) == 3) r_g2_mul_xabs<false>(S, X, P);
+  r_g2_psi(S, PSI, P);
+  r_export(S, X, 12);
+  if (r_tid() == 0) {
+    g2j acc, ps;
+    acc.x = fp2{r_fp_of_staged(S, 0), r_fp_of_staged(S, 1)};
+    acc.y = fp2{r_fp_of_staged(S, 2), r_fp_of_staged(S, 3)};
+    acc.z = fp2{r_fp_of_staged(S, 4), r_fp_of_staged(S, 5)};
+    ps.x = fp2{r_fp_of_staged(S, 6), r_fp_of_staged(S, 7)};
+    ps.y = fp2{r_fp_of_staged(S, 8), r_fp_of_staged(S, 9)};
+    ps.z = fp2{r_fp_of_staged(S, 10), r_fp_of_staged(S, 11)};
+    bool ok = !jac_is_inf(acc);  // psi(P) is finite
+    if (ok) ok = jac_eq(ps, jac_neg(acc));
+    if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
+  }
+}
+#endif  // LB_KG
+
 // ---------------------------------------------------------------- hash_to_G2
 // ---- expand_message_xmd for a 32-byte message at word level (no byte buffers: the byte-wise
 // SHA-256 message builder kept its buffers on the stack, ~1.5 KB of private segment per lane).

@@ -940,6 +940,13 @@ static __device__ const r_opl LBR_OPS_FE_A0 = r_ops_fe_tail(LBR_A(0), LBR_A(0));
 static __device__ const r_opl LBR_OPS_ML_A0 = r_ops_miller(LBR_A(0));
 static __device__ const r_opl LBR_OPS_ML_A7 = r_ops_miller(LBR_A(7));
 static __device__ const r_opl LBR_OPS_HASH = r_ops_hash_finish(LBR_A(4), LBR_A(3));
+// [|x|] p for the signature subgroup check (k_sig_subgroup_row): A(4) = [|x|] A(3), fast additions
+constexpr r_opl r_ops_xladder(int dst, int p) {
+  r_opl o;
+  o.g2_mul_xabs(dst, p);
+  return o;
+}
+static __device__ const r_opl LBR_OPS_XLADDER = r_ops_xladder(LBR_A(4), LBR_A(3));
 static_assert(r_ops_fe_tail(LBR_A(0), LBR_A(0)).n <= LBR_MAX_OPS && r_ops_hash_finish(LBR_A(4), LBR_A(3)).n <= LBR_MAX_OPS,
               "lb_row.h: op list size");
 

@@ -518,13 +518,16 @@ def small_order_signatures():
     return out
 
 
-@pytest.mark.parametrize("g8_max", ["0", str(1 << 31)])
-def test_small_order_signatures_not_in_group(monkeypatch, g8_max):
-    """Both subgroup-check kernels (one lane per set: k_sig_subgroup; 8 lanes: k_sig_subgroup_g8)
-    reject points of small order with BLST_POINT_NOT_IN_GROUP, in one batch beside valid sets."""
+@pytest.mark.parametrize("g8_max,row_fe", [("0", "0"), (str(1 << 31), "0"), (str(1 << 31), "1")])
+def test_small_order_signatures_not_in_group(monkeypatch, g8_max, row_fe):
+    """Every subgroup-check kernel (one lane per set: k_sig_subgroup; 8 lanes: k_sig_subgroup_g8;
+    a row workgroup per set: k_sig_subgroup_row, whose fast ladder meets the exceptional cases of
+    small-order points and reruns with the tested additions) rejects points of small order with
+    BLST_POINT_NOT_IN_GROUP, in one batch beside valid sets."""
     from lodestar_amd import _native as N
     from lodestar_amd.engine import Engine
     monkeypatch.setenv("LB_SUBGROUP_G8_MAX", g8_max)
+    monkeypatch.setenv("LB_ROW_FE", row_fe)
     cases, jobs = case_jobs()
     valid = jobs[[c["name"] for c in cases].index("single_valid_0")]
     pk, root = valid[0].pubkeys, valid[0].signing_root

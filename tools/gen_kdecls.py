@@ -41,7 +41,7 @@ GROUPS = {
     9: ["k_msm_buckets_g8", "k_msm_window_g8", "k_msm_horner_g8", "k_sig_blind_g8", "k_sig_blind", "k_g2_sum64", "k_sig_unblinded", "k_g2_sum_g8"],
     10: ["k_miller_row", "k_tree_up_row"],
     11: ["k_ml_S_row", "k_root_check_row", "k_root_partial_row", "k_partials_check_row"],
-    12: ["k_hash_finish_row", "k_sig_blind_row"],
+    12: ["k_hash_finish_row", "k_sig_blind_row", "k_sig_subgroup_row"],
     13: ["k_hash_map_row", "k_decompress_sigs_row"],
 }
 N_GROUPS = len(GROUPS)
