@@ -122,6 +122,7 @@ struct lb_engine {
   hipStream_t hp[3] = {nullptr, nullptr, nullptr};
   uint32_t prio_max = 0;
   hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr, ev_pk = nullptr;
+  hipEvent_t ev_pkst = nullptr;  // the pubkey statuses (k_pk_blind mode 1), before the ladder
   std::mutex mu;
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
@@ -475,6 +476,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_dec, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_pk, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_pkst, hipEventDisableTiming);
   for (int i = 0; i < kStages; i++) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
@@ -530,6 +532,7 @@ void lb_engine_destroy(lb_engine* e) {
   hipEventDestroy(e->ev_fork);
   hipEventDestroy(e->ev_dec);
   hipEventDestroy(e->ev_pk);
+  if (e->ev_pkst) hipEventDestroy(e->ev_pkst);
   hipStreamSynchronize(e->stream2);
   hipStreamSynchronize(e->stream3);
   if (e->scratch) delete e->scratch;
@@ -945,11 +948,17 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, s3, nc, b->d_chunk_lo.as<uint32_t>(),
                            b->d_pks.as<uint8_t>(), e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>());
     }
+    // on its own stream the pubkey side splits: the aggregates' statuses (what the job statuses
+    // and so the S side need) first, then the r PK ladder (only the per-root sums need it)
+    const bool pk_split = s3 != s2;
     {
       stage_scope sc(e, ST_PK_BLIND, s3);
-      hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s3, n, nc, b->d_set_chunk_off.as<uint32_t>(),
-                         e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
-                         e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
+      for (uint32_t mode = pk_split ? 1u : 0u; mode <= (pk_split ? 2u : 0u); mode++) {
+        hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s3, n, nc, b->d_set_chunk_off.as<uint32_t>(),
+                           e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
+                           e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>(), mode);
+        if (mode == 1u) LB_HIP(hipEventRecord(e->ev_pkst, s3));
+      }
     }
     LB_HIP(hipEventRecord(e->ev_pk, s3));
     // signatures: decoded while s1 groups and hashes the messages
@@ -974,7 +983,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       else
         hipLaunchKernelGGL(k_sig_subgroup, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
-      LB_HIP(hipStreamWaitEvent(s2, e->ev_pk, 0));  // job statuses need the pubkey statuses
+      LB_HIP(hipStreamWaitEvent(s2, pk_split ? e->ev_pkst : e->ev_pk, 0));  // job statuses need the pubkey statuses
       hipLaunchKernelGGL(k_job_status, dim3(nblk(nj)), dim3(LB_TPB), 0, s2, nj, b->d_job_off.as<uint32_t>(),
                          e->sig_status.as<int32_t>(), e->pk_status.as<int32_t>(), e->job_status.as<int32_t>(),
                          e->set_live.as<uint32_t>());
@@ -1109,6 +1118,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       LB_HIP(per_root_chain(e, n, nuh, mu, e->set_spec.as<uint32_t>()));
     } else {
       LB_HIP(hipStreamWaitEvent(s1, e->ev_dec, 0));
+      LB_HIP(hipStreamWaitEvent(s1, e->ev_pk, 0));  // r PK (the decode's wait covered the statuses only)
       LB_HIP(per_root_chain(e, n, nuh, mu, e->set_live.as<uint32_t>()));
     }
   } else {

@@ -952,11 +952,29 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
                                                          uint32_t* __restrict__ pk_aff,
                                                          const uint64_t* __restrict__ scalars,
                                                          uint32_t* __restrict__ rpk,
-                                                         int32_t* __restrict__ pk_status) {
+                                                         int32_t* __restrict__ pk_status, uint32_t mode) {
+  // mode 0: all; 1: the aggregate, its status and affine form only (pk_status, pk_aff: what the
+  // job statuses need, ahead of the ladder); 2: the ladder only, from mode 1's pk_status / pk_aff
   const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
   const bool act = i < n;
   int st = LB_ERR_ARGUMENT;
   g1j rj = jac_infinity<fp>();
+  if (mode == 2) {  // uniform
+    if (!act) return;
+    st = pk_status[i];
+    if (st == LB_OK) {
+      const g1a pk = soa_ld<g1a>(pk_aff, n, i);
+      const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
+      const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
+#if LB_G1_INL
+      rj = jac_as<fp>(jac_mul_glv_i<fpi, true>(aff_as<fpi>(pk), aff_as<fpi>(t2), aff_as<fpi>(t3), scalars[i]));
+#else
+      rj = jac_mul_glv_i<fp, true>(pk, t2, t3, scalars[i]);
+#endif
+    }
+    aos_st(rpk, i, rj);
+    return;
+  }
   if (act) {
     uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
     st = (c0 == c1) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
@@ -982,6 +1000,12 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   } else {
     pk.x = rj.x;
     pk.y = rj.y;
+  }
+  if (mode == 1) {  // uniform
+    if (!act) return;
+    if (ok) soa_st(pk_aff, n, i, pk);
+    pk_status[i] = st;
+    return;
   }
   if (ok) {
     // r * PK with r = lo + hi * lambda: t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y)
