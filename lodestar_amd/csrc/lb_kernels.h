@@ -1213,13 +1213,15 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // members summed per lane in k_gsum_chunks: 4 with the k_gsum_tree levels for a batch alone on
 // the device (latency), 32 with the chunk sums added per root on one lane under load (the tree's
 // wide launches cost the batches in flight throughput, profiles/r5_row_ab.txt); lb_engine.hip
+#ifndef LB_GROUP_CHUNK_ALONE
 #define LB_GROUP_CHUNK_ALONE 4
+#endif
 #define LB_GROUP_CHUNK 32
+#ifndef LB_GSUM_FAN
 #define LB_GSUM_FAN 4     // partial sums combined per lane and level in k_gsum_tree
-#ifndef LB_MSM_CHUNK
+#endif
 #ifndef LB_MSM_CHUNK
 #define LB_MSM_CHUNK 16  // bucket members summed per lane in k_msm_chunks (the batch MSM's serial chain)
-#endif
 #endif
 __device__ __forceinline__ bool msg_eq(const uint8_t* __restrict__ msgs, uint32_t a, uint32_t b) {
   const uint4* x = reinterpret_cast<const uint4*>(msgs + (size_t)32 * a);
