@@ -133,7 +133,7 @@ struct lb_engine {
   uint32_t gmax_chunks = 0;  // chunks of the largest root (the k_gsum_tree levels), read back with n_u
   bool gsum_tree = true;     // LB_GSUM_TREE=0: the chunk sums added serially per root (A/B)
   // this pipeline run's forms: `alone` (device_alone at its start) picks the latency forms -- the
-  // row engine (row_fe: LB_ROW_FE=0 disables it) and the per-root sum tree over 4-member chunks
+  // row engine (row_fe: LB_ROW_FE=0 disables it) and the per-root sum tree over 8-member chunks
   bool alone = false, row_fe = true;
   uint32_t gchunk = LB_GROUP_CHUNK;
   // bucket MSM for sum r_i sig_i (k_msm_*)

@@ -1210,11 +1210,11 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 // slot 0xffffffff), probed from a keyed hash of the root (key from the engine's CSPRNG, so crafted
 // roots cannot be aimed at one probe chain); equality is decided on all 32 bytes.  A slot, once
 // claimed by compare-and-swap, never changes, so a loser can compare against its owner at once.
-// members summed per lane in k_gsum_chunks: 4 with the k_gsum_tree levels for a batch alone on
+// members summed per lane in k_gsum_chunks: 8 with the k_gsum_tree levels for a batch alone on
 // the device (latency), 32 with the chunk sums added per root on one lane under load (the tree's
 // wide launches cost the batches in flight throughput, profiles/r5_row_ab.txt); lb_engine.hip
 #ifndef LB_GROUP_CHUNK_ALONE
-#define LB_GROUP_CHUNK_ALONE 4
+#define LB_GROUP_CHUNK_ALONE 8
 #endif
 #define LB_GROUP_CHUNK 32
 #ifndef LB_GSUM_FAN
