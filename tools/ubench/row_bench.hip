@@ -123,6 +123,26 @@ __global__ void __launch_bounds__(NT) k_lds_chase(int iters, uint64_t* out, int*
   if (threadIdx.x == 0) out[0] = t1 - t0;
   sink[threadIdx.x] = p;
 }
+// pieces of k_hash_map_row's lone-lane part (one wave; every lane the same item)
+template <int OP>
+__global__ void __launch_bounds__(64) k_h2c_parts(int iters, uint64_t* out, uint32_t* sink) {
+  uint32_t M[8];
+  for (int i = 0; i < 8; i++) M[i] = 0x01020304u * (i + 1) + threadIdx.x / 16;
+  fp2 u = hash_to_field_u(M, 0);
+  uint32_t acc = 0;
+  const uint64_t t0 = rt();
+  for (int it = 0; it < iters; it++) {
+    if (OP == 0) { u = hash_to_field_u(M, 0); M[0] ^= u.c0.v[0]; }
+    if (OP == 1) { acc += fp_is_square_i(fp_add(u.c0, fp_one())) ? 1 : 0; u.c0 = fp_add(u.c0, fp_one()); }
+    if (OP == 2) { u = fp2_inv_i(u); }
+    if (OP == 3) { const g2j r = map_to_curve_g2_i<true>(u); u.c0 = fp_add(u.c0, r.x.c0); }
+    if (OP == 4) { u.c0 = r1_pow_const(u.c0, LB_EXP_SQRT, 378); }
+    if (OP == 5) { u = fp2_mul(u, u); }
+  }
+  const uint64_t t1 = rt();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = u.c0.v[0] + u.c1.v[3] + acc;
+}
 // synthetic one-phase programs written over the image at offset 0: the cost of a phase's parts
 template <int V>
 __global__ void __launch_bounds__(LBR_NT) k_synth(int iters, uint64_t* out) {
@@ -372,6 +392,12 @@ int main() {
   }
   run("lds chase (64 thr)", [&](int n) { hipLaunchKernelGGL(k_lds_chase<64>, dim3(1), dim3(64), 0, 0, n, d, sink); }, 10000);
   run("lds chase (1024 thr)", [&](int n) { hipLaunchKernelGGL(k_lds_chase<1024>, dim3(1), dim3(1024), 0, 0, n, d, sink); }, 10000);
+  run("h2c hash_to_field", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<0>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 20);
+  run("h2c is_square (Jacobi)", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<1>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 20);
+  run("h2c fp2 inverse", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<2>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 20);
+  run("h2c map_to_curve (row pows)", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<3>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 5);
+  run("h2c one row pow", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<4>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 10);
+  run("h2c fp2 mul (lane)", [&](int n) { hipLaunchKernelGGL(k_h2c_parts<5>, dim3(1), dim3(64), 0, 0, n, d, (uint32_t*)sink); }, 200);
   run("synth P1 plain", [&](int n) { hipLaunchKernelGGL(k_synth<0>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth P1 8+8 terms", [&](int n) { hipLaunchKernelGGL(k_synth<1>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
   run("synth P1 8+8 reduce", [&](int n) { hipLaunchKernelGGL(k_synth<2>, dim3(1), dim3(LBR_NT), 0, 0, n, d); }, 1000);
