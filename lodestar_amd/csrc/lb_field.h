@@ -759,6 +759,71 @@ LB_HD uint64_t lb_bits64(const uint32_t* w, int off, int nbits) {  // bits [off,
   }
   return nbits >= 64 ? x : (x & ((1ULL << nbits) - 1));
 }
+// The Jacobi symbol by "posdivsteps" (the Jacobi variant of the divsteps above, as in
+// libsecp256k1's modinv64 jacobi): f, g stay non-negative (a swap does not negate), and the
+// symbol's sign bit in jac flips when g loses an odd power of 2 while f = 3, 5 mod 8, and when a
+// swap meets f = g = 3 mod 4.  ~20 jumps of 62 steps against the binary algorithm's ~760
+// word-array iterations (hash_to_G2's is_square: ~184 us -> tens of us on a lone lane).
+LB_HD int64_t lb_posdivsteps62(int64_t eta, uint64_t f0, uint64_t g0, int64_t t[4], int& jac) {
+  uint64_t u = 1, v = 0, q = 0, r = 1, f = f0, g = g0, m, w;
+  int i = 62;
+  for (;;) {
+    const int zeros = lb_ctz64(g | (~0ULL << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    jac ^= (int)(zeros & ((f >> 1) ^ (f >> 2)));
+    if (i == 0) break;
+    int limit;
+    if (eta < 0) {  // swap (no negation)
+      uint64_t tmp;
+      eta = -eta;
+      tmp = f; f = g; g = tmp;
+      tmp = u; u = q; q = tmp;
+      tmp = v; v = r; r = tmp;
+      jac ^= (int)((f & g) >> 1);
+      limit = (int)eta + 1 > i ? i : (int)eta + 1;
+      m = (~0ULL >> (64 - limit)) & 63u;
+      w = (f * g * (f * f - 2)) & m;
+    } else {
+      limit = (int)eta + 1 > i ? i : (int)eta + 1;
+      m = (~0ULL >> (64 - limit)) & 15u;
+      w = f + (((f + 1) & 4) << 1);
+      w = ((uint64_t)0 - w * g) & m;
+    }
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t[0] = (int64_t)u;
+  t[1] = (int64_t)v;
+  t[2] = (int64_t)q;
+  t[3] = (int64_t)r;
+  return eta;
+}
+// (x | p) for x in [0, p) given as 12 words (0 counts as a square): 1 square, 0 non-square,
+// -1 not settled within the jump budget (the caller falls back to the binary algorithm)
+LB_HD int fp_is_square_sg(const fp& x) {
+  if (fp_is_zero(x)) return 1;
+  lb_s62 f = lb_s62_p(), g;
+  LB_UNROLL for (int i = 0; i < 7; i++) g.v[i] = (int64_t)lb_bits64(x.v, 62 * i, 62);
+  int64_t eta = -1, t[4];
+  int jac = 0;
+  for (int it = 0; it < 60; it++) {
+    // 64 low bits (the symbol's updates read f mod 8 up to the 62nd step)
+    eta = lb_posdivsteps62(eta, (uint64_t)f.v[0] | ((uint64_t)f.v[1] << 62), (uint64_t)g.v[0] | ((uint64_t)g.v[1] << 62),
+                           t, jac);
+    lb_s62_update_fg(f, g, t);
+    if (f.v[0] == 1) {
+      int64_t any = 0;
+      LB_UNROLL for (int i = 1; i < 7; i++) any |= f.v[i];
+      if (any == 0) return (jac & 1) ? 0 : 1;
+    }
+  }
+  return -1;
+}
 // plain a in [0, p) -> a^-1 mod p (plain), 0 -> 0
 LB_HD fp fp_inv_plain_by_i(const fp& a) {
   if (fp_is_zero(a)) return a;

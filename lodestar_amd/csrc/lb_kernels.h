@@ -439,7 +439,8 @@ __device__ __forceinline__ fp2 fp2_inv_i(const fp2& a) {
   const fp ni = fp_inv_i(fp_add(fp_sqr(a.c0), fp_sqr(a.c1)));
   return fp2{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
 }
-__device__ __forceinline__ bool fp_is_square_i(const fp& a) {
+// binary Jacobi symbol (the fallback when posdivsteps has not settled)
+__device__ __forceinline__ bool fp_is_square_bin_i(const fp& a) {
   if (fp_is_zero(a)) return true;
   uint32_t u[12], v[12];
   const uint32_t Pl[12] = {LB_P0, LB_P1, LB_P2, LB_P3, LB_P4, LB_P5, LB_P6, LB_P7, LB_P8, LB_P9, LB_P10, LB_P11};
@@ -474,6 +475,16 @@ __device__ __forceinline__ bool fp_is_square_i(const fp& a) {
     LB_UNROLL for (int j = 0; j < 12; j++) zero &= u[j] == 0;
     if (zero) return false;
   }
+}
+#ifndef LB_JAC_SG
+#define LB_JAC_SG 1  // 0: the binary Jacobi symbol only (A/B)
+#endif
+__device__ __forceinline__ bool fp_is_square_i(const fp& a) {
+  if (LB_JAC_SG) {
+    const int s = fp_is_square_sg(a);  // (aR | p) = (a | p): R = 2^384 is a square
+    if (s >= 0) return s == 1;
+  }
+  return fp_is_square_bin_i(a);
 }
 // map_to_curve_g2 (SSWU + 3-isogeny, lb_h2c.h) with the inline pieces above; ROW: the square
 // root's two exponentiations on the lane's 16-lane row (r1_pow_const; every lane of the row runs
