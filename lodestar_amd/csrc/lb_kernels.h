@@ -973,7 +973,10 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   if (mode == 2) {  // uniform
     if (!act) return;
     st = pk_status[i];
-    if (st == LB_OK) {
+    if (st == LB_OK && scalars[i] == 1) {  // the unblinded 1-set call: r PK = PK, kept affine (Z = 1)
+      const g1a pk = soa_ld<g1a>(pk_aff, n, i);
+      rj = g1j{pk.x, pk.y, fp_one()};
+    } else if (st == LB_OK) {
       const g1a pk = soa_ld<g1a>(pk_aff, n, i);
       const g1a t2{fp_mul(pk.x, fp_load(LB_GLV_BETA)), pk.y};
       const g1a t3{fp_mul(pk.x, fp_load(LB_GLV_BETA2)), fp_neg(pk.y)};
@@ -2543,7 +2546,9 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
       acc = soa_ld<g1j>(gacc, n, gch[u]);
   }
   const bool zero = jac_is_inf(acc);
-  const fp zi = fp_inv_block(act && !zero ? acc.z : fp_one());
+  // a block whose sums all have Z = 1 (the unblinded 1-set call's affine PK) skips the inversion
+  const bool need = act && !zero && !fp_eq(acc.z, fp_one());
+  const fp zi = __syncthreads_or(need) ? fp_inv_block(need ? acc.z : fp_one()) : fp_one();
   if (!act) return;
   g1a a;
   if (zero) {
