@@ -1015,8 +1015,14 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
       // distinct-root count to the host: the per-root kernels below are launched over it (a
       // launch over the set count would size their private-segment scratch for n lanes)
-      LB_HIP(hipMemcpyAsync(e->h_nu, e->n_u.p, 8, hipMemcpyDeviceToHost, s1));
-      LB_HIP(hipStreamSynchronize(s1));
+      // (one set: one root of one chunk, known without the round trip)
+      if (n == 1) {
+        e->h_nu[0] = 1;
+        e->h_nu[1] = 1;
+      } else {
+        LB_HIP(hipMemcpyAsync(e->h_nu, e->n_u.p, 8, hipMemcpyDeviceToHost, s1));
+        LB_HIP(hipStreamSynchronize(s1));
+      }
     }
     const uint32_t nuh = e->h_nu[0];
     e->gmax_chunks = e->h_nu[1];
