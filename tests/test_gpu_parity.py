@@ -470,11 +470,16 @@ def test_verify_jobs_workspace_reuse_and_indexed(engine):
     p = W.PackedJobs(job_off=wl.packed.job_off, pk_off=wl.packed.pk_off, pubkeys=wl.packed.pubkeys,
                      msgs=wl.packed.msgs, sigs=wl.packed.sigs, sig_sizes=None)   # 96-byte keys
     ip = W.indexed_for(engine, wl)                                              # table indices
+    # uploads up to 1 MiB go up as one staged copy into views of one arena (lb_engine.hip
+    # batch_fill), larger ones as owned buffers: alternate the two on the same workspace
+    big = W.make(engine, "c3", slots=1)
+    bip = W.indexed_for(engine, big)
     for _ in range(2):
         assert engine.verify_jobs_packed(p) == list(wl.expected)
         assert engine.verify_jobs_packed(ip) == list(wl.expected)
         small = make_batch(engine, 3, seed=41, invalid={1})
         assert engine.verify_jobs(small) == [1, 0, 1]
+        assert engine.verify_jobs_packed(bip) == list(big.expected)
 
 
 def test_indexed_null_indices_only_without_keys(engine):
