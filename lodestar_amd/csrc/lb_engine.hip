@@ -1048,27 +1048,35 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // ---- s1: group the sets by signing root
     {
       stage_scope sc(e, ST_DEDUP, s1);
-      LB_HIP(hipMemsetAsync(e->msg_tab.p, 0xff, (size_t)cap * 4, s1));
-      LB_HIP(hipMemsetAsync(e->n_u.p, 0, 4, s1));
-      LB_HIP(hipMemsetAsync(e->gcnt.p, 0, (size_t)n * 4, s1));
-      hipLaunchKernelGGL(k_msg_insert, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(), e->msg_key,
-                         cap, e->msg_tab.as<uint32_t>(), e->rep_of.as<uint32_t>());
-      if (e->root_shuffle)
-        hipLaunchKernelGGL(k_msg_uid, dim3(nblk(cap)), dim3(LB_TPB), 0, s1, cap, e->msg_tab.as<uint32_t>(),
-                           e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
-      else
-        hipLaunchKernelGGL(k_msg_uid_input, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
-                           e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
-                         e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
-                         e->gpos.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gchunk, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
-                         e->gch.as<uint32_t>(), nullptr, nullptr, nullptr, e->n_u.as<uint32_t>() + 1);
-      hipLaunchKernelGGL(k_chunk_fill, dim3(nblk(n + n / e->gchunk + 1)), dim3(LB_TPB), 0, s1, nu,
-                         e->gchunk, e->goff.as<uint32_t>(), e->gch.as<uint32_t>(),
-                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>());
-      hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
-                         e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
+      if (n == 1) {
+        hipLaunchKernelGGL(k_dedup_one, dim3(1), dim3(64), 0, s1, e->rep_of.as<uint32_t>(), e->uid_of.as<uint32_t>(),
+                           e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>(), e->set_uid.as<uint32_t>(),
+                           e->gcnt.as<uint32_t>(), e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->gch.as<uint32_t>(),
+                           e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>(),
+                           e->members.as<uint32_t>());
+      } else {
+        LB_HIP(hipMemsetAsync(e->msg_tab.p, 0xff, (size_t)cap * 4, s1));
+        LB_HIP(hipMemsetAsync(e->n_u.p, 0, 4, s1));
+        LB_HIP(hipMemsetAsync(e->gcnt.p, 0, (size_t)n * 4, s1));
+        hipLaunchKernelGGL(k_msg_insert, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, b->d_msgs.as<uint8_t>(), e->msg_key,
+                           cap, e->msg_tab.as<uint32_t>(), e->rep_of.as<uint32_t>());
+        if (e->root_shuffle)
+          hipLaunchKernelGGL(k_msg_uid, dim3(nblk(cap)), dim3(LB_TPB), 0, s1, cap, e->msg_tab.as<uint32_t>(),
+                             e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
+        else
+          hipLaunchKernelGGL(k_msg_uid_input, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
+                             e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
+        hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
+                           e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
+                           e->gpos.as<uint32_t>());
+        hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gchunk, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
+                           e->gch.as<uint32_t>(), nullptr, nullptr, nullptr, e->n_u.as<uint32_t>() + 1);
+        hipLaunchKernelGGL(k_chunk_fill, dim3(nblk(n + n / e->gchunk + 1)), dim3(LB_TPB), 0, s1, nu,
+                           e->gchunk, e->goff.as<uint32_t>(), e->gch.as<uint32_t>(),
+                           e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>());
+        hipLaunchKernelGGL(k_msg_scatter, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->set_uid.as<uint32_t>(),
+                           e->gpos.as<uint32_t>(), e->goff.as<uint32_t>(), e->members.as<uint32_t>());
+      }
       // distinct-root count to the host: the per-root kernels below are launched over it (a
       // launch over the set count would size their private-segment scratch for n lanes)
       // (one set: one root of one chunk, known without the round trip)

@@ -1274,6 +1274,35 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_insert(uint32_t n, const uint8_t
   rep_of[i] = rep;
 }
 #endif  // LB_KG
+// The grouping of a ONE-set batch (what k_msg_insert .. k_msg_scatter produce for n = 1: one
+// root of one member in one chunk) in one launch instead of three fills and six kernels
+#if LB_KG(0)
+__global__ void __launch_bounds__(64) k_dedup_one(uint32_t* __restrict__ rep_of, uint32_t* __restrict__ uid_of,
+                                                  uint32_t* __restrict__ uniq_set, uint32_t* __restrict__ n_u,
+                                                  uint32_t* __restrict__ set_uid, uint32_t* __restrict__ cnt,
+                                                  uint32_t* __restrict__ pos, uint32_t* __restrict__ goff,
+                                                  uint32_t* __restrict__ gch, uint32_t* __restrict__ chunk_beg,
+                                                  uint32_t* __restrict__ chunk_end, uint32_t* __restrict__ chunk_root,
+                                                  uint32_t* __restrict__ members) {
+  if (threadIdx.x != 0) return;
+  rep_of[0] = 0;
+  uid_of[0] = 0;
+  uniq_set[0] = 0;
+  n_u[0] = 1;  // distinct roots
+  n_u[1] = 1;  // chunks of the largest root
+  set_uid[0] = 0;
+  cnt[0] = 1;
+  pos[0] = 0;
+  goff[0] = 0;
+  goff[1] = 1;
+  gch[0] = 0;
+  gch[1] = 1;
+  chunk_beg[0] = 0;
+  chunk_end[0] = 1;
+  chunk_root[0] = 0;
+  members[0] = 0;
+}
+#endif  // LB_KG
 // Unique-message ids in input order (the first set of each root, LB_ROOT_SHUFFLE=0)
 #if LB_KG(0)
 __global__ void __launch_bounds__(LB_TPB) k_msg_uid_input(uint32_t n, const uint32_t* __restrict__ rep_of,

@@ -24,7 +24,7 @@ OUT = os.path.join(CSRC, "lb_kdecl.h")
 # kernel -> translation-unit group (balanced by measured compile time; the one-lane per-root and
 # decode kernels are the slow ones)
 GROUPS = {
-    0: ["k_decompress_sigs", "k_table_fill", "k_g1_decompress", "k_aggregate", "k_msg_insert", "k_msg_uid_input",
+    0: ["k_decompress_sigs", "k_table_fill", "k_g1_decompress", "k_aggregate", "k_msg_insert", "k_dedup_one", "k_msg_uid_input",
         "k_msg_uid", "k_msg_count", "k_msg_scan", "k_chunk_fill", "k_msg_scatter", "k_job_status", "k_spec_live", "k_live_mismatch",
         "k_set_one", "k_g2_set_inf"],
     1: ["k_sig_subgroup", "k_sig_subgroup_g8", "k_sig_agg_chunks", "k_sig_agg_groups"],
