@@ -78,11 +78,17 @@ int32_t lb_engine_create(int32_t device, lb_engine** out);
  * reference's verifyOnMainThread path, multithread/index.ts:138-151): its streams run on a
  * reserved set of CUs (LB_LATENCY_CUS, default 8) and it always takes the small-batch latency
  * forms; engines created AFTER it on the device run on the remaining CUs, so a 1-set call does not
- * queue behind the pool's batches.  Create the latency engine first.
+ * queue behind the pool's batches.  Create the latency engine first (engines created before it keep
+ * every CU; a warning is printed).  The partition lasts while a latency engine exists: engines
+ * created after the last one is destroyed get the whole device again.  CU-masked streams are
+ * blocking streams (they synchronise with the legacy null stream).
  */
 #define LB_ENGINE_LATENCY 1u
 int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out);
 void lb_engine_destroy(lb_engine* e);
+/* CUs the engine's streams may use: the device's count, the reserved CUs for a latency engine, or
+ * the rest while a partition exists.  0 for NULL. */
+int32_t lb_engine_cu_count(const lb_engine* e);
 
 /*
  * Upload one batch of jobs into device memory (copies; the caller keeps its buffers).

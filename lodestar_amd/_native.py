@@ -46,6 +46,7 @@ SIGNATURES = {
     "lb_engine_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "lb_engine_create_ex": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     "lb_engine_destroy": (None, [_vp]),
+    "lb_engine_cu_count": (ctypes.c_int32, [_vp]),
     "lb_batch_create": (ctypes.c_int32, [_vp, ctypes.c_uint32, _u32p, _u32p, _u8p, _u8p, _u8p, _u32p,
                                          ctypes.POINTER(_vp)]),
     "lb_batch_destroy": (None, [_vp]),

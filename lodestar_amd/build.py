@@ -72,7 +72,9 @@ def build_lib(force=False, verbose=True, extra_flags=(), out=None):
     order = [u for u in units if u[1] in ("3", "6", "8", "9", "7")] + [u for u in units if u[1] not in ("3", "6", "8", "9", "7")]
     running, failed = [], []
     t0 = time.time()
-    pend = list(order)
+    # per-unit staleness: the kernel groups do not include lb_engine.hip (host code + launches)
+    kdeps = [d for d in _deps() if os.path.basename(d) != "lb_engine.hip"]
+    pend = [u for u in order if force or extra_flags or _stale(u[2], _deps() if u[1] == "99" else kdeps)]
     while pend or running:
         while pend and len(running) < _jobs():
             src, g, obj = pend.pop(0)
@@ -157,7 +159,7 @@ def build_napi(force=False, verbose=True):
         return None
     if not force and not _stale(NAPI, [src, LIB, os.path.join(INC, "lodestar_bls.h")]):
         return NAPI
-    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-I/usr/include/node", "-I" + INC, src, "-o", NAPI + ".tmp",
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-pthread", "-I/usr/include/node", "-I" + INC, src, "-o", NAPI + ".tmp",
            "-L" + os.path.dirname(LIB), "-llodestar_bls", "-Wl,-rpath,$ORIGIN/.."]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)

@@ -127,6 +127,7 @@ struct lb_engine {
   // LB_ENGINE_LATENCY (lb_engine_create_ex): streams confined to the device's reserved CUs, the
   // latency forms always (the partition keeps every other engine off those CUs)
   bool latency = false;
+  int n_cus = 0;  // CUs its streams may use (the whole device, or one side of the partition)
   hipStream_t stream = nullptr;   // s1
   hipStream_t stream2 = nullptr;  // s2
   hipStream_t stream3 = nullptr;  // s3: pubkey aggregation + blinding, beside the signature decode
@@ -146,10 +147,19 @@ struct lb_engine {
   dbuf msg_tab, rep_of, uid_of, uniq_set, n_u, set_uid, gcnt, gpos, goff, gch, chunk_beg, chunk_end, members,
       set_live, gacc, gp_aff, gp_inf, chunk_root;
   uint32_t gmax_chunks = 0;  // chunks of the largest root (the k_gsum_tree levels), read back with n_u
+  // under load (not alone) the per-root sums fold the blinding in, one Straus chain per chunk
+  // (k_gsum_straus over pk3) instead of k_pk_blind's per-set ladder + the chunk sums; the per-set
+  // r PK (rpk) are then computed only if a search needs them (rpk_stale).  LB_GSUM_STRAUS=0: off
+  bool straus = true, straus_run = false, rpk_stale = false;
+  // a batch alone: the per-root sums' chunks combined by a segmented shuffle tree in one launch
+  // (k_gsum_wave, chunks of LB_GROUP_CHUNK_WAVE) instead of the k_gsum_tree launches; LB_GSUM_WAVE=0
+  bool gsum_wave = true;
+  dbuf pk3;
   bool gsum_tree = true;     // LB_GSUM_TREE=0: the chunk sums added serially per root (A/B)
   // this pipeline run's forms: `alone` (device_alone at its start) picks the latency forms -- the
   // row engine (row_fe: LB_ROW_FE=0 disables it) and the per-root sum tree over 8-member chunks
   bool alone = false, row_fe = true;
+  int alone_force = -1;  // LB_ALONE=1 / 0 pins device_alone() (tests: the latency forms must run), -1 by load
   uint32_t gchunk = LB_GROUP_CHUNK;
   // bucket MSM for sum r_i sig_i (k_msm_*)
   dbuf sig_aos, bcnt, bcursor, boff, bch, bchunk_beg, bchunk_end, bmembers, bacc, bsum, wsum;
@@ -274,9 +284,12 @@ static exit_rec g_device_exit[64][2];
 static int64_t lb_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-// CUs reserved for latency engines per device (0: no partition yet); engines created while a
-// partition exists run on the complement.  LB_LATENCY_CUS (default 8 of the device's CUs).
+// CUs reserved for latency engines per device (0: no partition); engines created while a
+// partition exists run on the complement.  LB_LATENCY_CUS (default 8 of the device's CUs).  The
+// partition lives as long as a latency engine does (g_latency_live counts them): after the last
+// one is destroyed, engines created later get the whole device again (round-5 ADVICE).
 static int g_latency_cus[64];
+static int g_latency_live[64];
 struct busy_scope {
   int dev;
   const void* eng;
@@ -305,6 +318,7 @@ struct busy_scope {
 template <class E>
 static bool device_alone(const E* e) {
   if (e->latency) return true;  // its reserved CUs run nothing else
+  if (e->alone_force >= 0) return e->alone_force != 0;
   if (g_device_busy[e->device].load(std::memory_order_relaxed) > 1) return false;
   int64_t other;
   {
@@ -333,9 +347,13 @@ static int max_engines_per_device() {
 static inline uint32_t nblk(uint32_t n) { return (n + LB_TPB - 1) / LB_TPB; }
 static inline uint32_t nblk_inv(uint32_t n) { return (n + LB_INV_TPB - 1) / LB_INV_TPB; }
 
-static int fill_scalars(lb_engine* e, uint32_t n, const uint64_t* user) {
+// unblinded: the verdict of this run covers exactly this batch (lb_batch_verify / lb_verify_jobs*),
+// so a 1-set batch may verify unblinded as Signature.verify does.  A partial product that is
+// multiplied with other ranks' partials (lb_batch_partial) is always blinded: two unblinded 1-set
+// partials sig_A + D and sig_B - D would cancel in the product (round-5 ADVICE).
+static int fill_scalars(lb_engine* e, uint32_t n, const uint64_t* user, bool unblinded) {
   e->h_scalars.resize(n);
-  if (!user && n == 1) {
+  if (!user && n == 1 && unblinded) {
     e->h_scalars[0] = 1;  // one set: verified unblinded (k_sig_unblinded), as Signature.verify
     return LB_OK;
   }
@@ -426,6 +444,8 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   if (const char* mw = getenv("LB_MILLER_WAVE_MAX")) e->miller_wave_max = (uint32_t)strtoul(mw, nullptr, 10);
   if (const char* rm = getenv("LB_ROW_MAX")) e->row_max = (uint32_t)strtoul(rm, nullptr, 10);
   if (const char* gt = getenv("LB_GSUM_TREE")) e->gsum_tree = std::atoi(gt) != 0;
+  if (const char* gs = getenv("LB_GSUM_STRAUS")) e->straus = std::atoi(gs) != 0;
+  if (const char* gw = getenv("LB_GSUM_WAVE")) e->gsum_wave = std::atoi(gw) != 0;
   if (const char* rf = getenv("LB_ROW_FE")) e->row_fe = std::atoi(rf) != 0;
   if (const char* pm = getenv("LB_PRIO_MAX")) e->prio_max = (uint32_t)strtoul(pm, nullptr, 10);
   if (const char* ml = getenv("LB_MILLER_LDS3_MAX")) e->miller_lds3_max = (uint32_t)strtoul(ml, nullptr, 10);
@@ -450,6 +470,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   if (const char* sm = getenv("LB_ROOT_SHUFFLE")) e->root_shuffle = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_MSM_G8")) e->msm_g8 = std::atoi(sm) != 0;
   if (const char* sm = getenv("LB_SPEC_GSUM")) e->spec_gsum = std::atoi(sm) != 0;
+  if (const char* al = getenv("LB_ALONE")) e->alone_force = std::atoi(al) != 0 ? 1 : 0;
   // CU partition: a latency engine's streams on the reserved CUs [0, R), every engine created
   // while a partition exists on [R, ncu)
   bool masked = false;
@@ -457,17 +478,26 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   {
     std::lock_guard<std::mutex> lk(g_engine_mu);
     const int ncu = prop.multiProcessorCount;
+    e->n_cus = ncu;
     if (flags & LB_ENGINE_LATENCY) {
       if (g_latency_cus[device] == 0) {
         const char* v = getenv("LB_LATENCY_CUS");
         const int r = v ? atoi(v) : 8;
         g_latency_cus[device] = std::max(1, std::min(r, ncu / 4));
+        // engines created before the partition keep the whole device (their streams exist):
+        // they share the reserved CUs, which only costs the latency engine its isolation
+        if (g_engine_count[device] > 1)
+          fprintf(stderr, "lodestar_bls: latency engine created after %d other engine(s) on device %d: "
+                  "those still run on every CU (create the latency engine first)\n", g_engine_count[device] - 1, device);
       }
+      g_latency_live[device]++;
       e->latency = true;
       mask = cu_mask(ncu, 0, g_latency_cus[device]);
+      e->n_cus = g_latency_cus[device];
       masked = true;
     } else if (g_latency_cus[device] > 0) {
       mask = cu_mask(ncu, g_latency_cus[device], ncu);
+      e->n_cus = ncu - g_latency_cus[device];
       masked = true;
     }
   }
@@ -483,9 +513,10 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
     if (e->stream2) hipStreamDestroy(e->stream2);
     if (e->stream3) hipStreamDestroy(e->stream3);
     if (e->h_nu) hipHostFree(e->h_nu);
-    delete e;
     std::lock_guard<std::mutex> lk(g_engine_mu);
     g_engine_count[device]--;
+    if (e->latency && --g_latency_live[device] == 0) g_latency_cus[device] = 0;
+    delete e;
     return LB_ERR_DEVICE;
   }
   hipEventCreateWithFlags(&e->ev_g1, hipEventDisableTiming);
@@ -498,8 +529,9 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
   }
-  // Reserve s1's scratch now, one engine at a time, for the largest private segment it can run
-  // (k_miller_lane<2>, 2.7 KB per lane): an empty dispatch over more waves than the device holds.
+  // Reserve the streams' scratch now, one engine at a time, for the largest private segments they
+  // can run (s1: k_miller_lane<2>, 2.7 KB per lane): empty dispatches over more waves than the
+  // device holds.
   // The runtime sizes a queue's scratch for the largest segment it has run, from one per-process
   // pool, and a queue that cannot grow it mid-run aborts asynchronously; growing it here, with the
   // stream synchronised, turns an exhausted pool into LB_ERR_DEVICE from lb_engine_create.
@@ -513,7 +545,22 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
                            nullptr, nullptr, nullptr, nullptr, nullptr);
         hipLaunchKernelGGL(k_hash_finish, dim3(4096), dim3(LB_INV_TPB), 0, e->stream, 0u, e->n_u.as<uint32_t>(),
                            nullptr, nullptr, nullptr, 0u);
-        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(e->stream) == hipSuccess;
+        // s2 and s3 the same way (round 6), each for the kernels with a private segment it runs,
+        // at their largest dispatch: s2 the signature decode over the whole device (472 B per
+        // lane), the 8-lane subgroup check and r_i sig_i of small batches (616 / 868 B); s3 the
+        // 96-byte-key chunk sums (584 B).  The rest of s2 / s3's kernels need less per lane and
+        // fewer lanes (resource table: DESIGN.md section 5.2).
+        hipLaunchKernelGGL(k_decompress_sigs, dim3(4096), dim3(LB_TPB), 0, e->stream2, 0u, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, nullptr);
+        // (one wave per 8 sets, at least one wave, at most 16 384: more than the device holds)
+        auto g8_waves = [](uint32_t sets) { return dim3(std::min<uint32_t>(16384u, std::max<uint32_t>(1u, sets / 8 + 1))); };
+        hipLaunchKernelGGL(k_sig_subgroup_g8, g8_waves(e->subgroup_g8_max), dim3(64), 0, e->stream2, 0u, nullptr, nullptr,
+                           nullptr);
+        hipLaunchKernelGGL(k_sig_blind_g8, g8_waves(e->small_s_g8_max), dim3(64), 0, e->stream2, 0u, nullptr, nullptr,
+                           nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_pk_chunks, dim3(4096), dim3(LB_TPB), 0, e->stream3, 0u, nullptr, nullptr, nullptr, nullptr);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(e->stream) == hipSuccess &&
+             hipStreamSynchronize(e->stream2) == hipSuccess && hipStreamSynchronize(e->stream3) == hipSuccess;
       }
     }
     if (!ok) {
@@ -567,9 +614,12 @@ void lb_engine_destroy(lb_engine* e) {
   {
     std::lock_guard<std::mutex> lk(g_engine_mu);
     g_engine_count[e->device]--;
+    if (e->latency && --g_latency_live[e->device] == 0) g_latency_cus[e->device] = 0;
   }
   delete e;
 }
+
+int32_t lb_engine_cu_count(const lb_engine* e) { return e ? e->n_cus : 0; }
 
 int32_t lb_engine_set_profiling(lb_engine* e, int32_t enable) {
   if (!e) return LB_ERR_ARGUMENT;
@@ -606,6 +656,7 @@ static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint
   for (uint32_t i = 0; i < n_sets; i++)
     if (set_pk_offsets[i + 1] < set_pk_offsets[i]) return LB_ERR_ARGUMENT;
   const uint32_t n_pks = set_pk_offsets[n_sets];
+  if (n_pks & LB_CHUNK_FIRST) return LB_ERR_ARGUMENT;  // key offsets are 31-bit (chunk flags)
   const bool indexed = pk_indices != nullptr;
   if ((n_sets && (!signing_roots || !signatures)) || (n_pks && !pubkeys && !indexed)) return LB_ERR_ARGUMENT;
   LB_HIP(hipSetDevice(e->device));
@@ -628,12 +679,13 @@ static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint
   chunk_lo.clear();
   for (uint32_t i = 0; i < n_sets; i++) {
     set_chunk_off[i] = (uint32_t)chunk_lo.size();
-    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK) chunk_lo.push_back(k);
+    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK)
+      chunk_lo.push_back(k | (k == set_pk_offsets[i] ? LB_CHUNK_FIRST : 0u));  // flag: the set's first chunk
   }
   set_chunk_off[n_sets] = (uint32_t)chunk_lo.size();
   b->n_chunks = (uint32_t)chunk_lo.size();
-  chunk_lo.push_back(n_pks);  // chunk c ends where chunk c+1 starts (chunks never span sets:
-  // a set's last chunk ends at the next set's first key, which is its own first chunk start)
+  chunk_lo.push_back(n_pks | LB_CHUNK_FIRST);  // chunk c ends where chunk c+1 starts (chunks never
+  // span sets: a set's last chunk ends at the next set's first key, which is its own first chunk start)
   b->indexed = indexed;
   struct part {
     dbuf* d;
@@ -682,6 +734,12 @@ static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint
   }
   if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
   if (r != hipSuccess) {
+    // no view may outlive a failed (re)allocation of the arena: the batch is left empty, so a
+    // later verify of it reads nothing (round-5 ADVICE)
+    for (const part& q : parts) q.d->release();
+    b->d_arena.release();
+    b->n_jobs = b->n_sets = b->n_pks = b->n_chunks = 0;
+    b->job_off.assign(1, 0u);
     fprintf(stderr, "lodestar_bls: batch upload failed: %s\n", hipGetErrorString(r));
     return LB_ERR_DEVICE;
   }
@@ -865,17 +923,27 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
     stage_scope sc(e, ST_GSUM, s1);
     // chunks of <= LB_GROUP_CHUNK members: at most nuh + n / LB_GROUP_CHUNK of them
     const uint32_t nch = nuh + n / e->gchunk;
-    hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu,
-                       e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
-                       e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
+    const bool wave = e->gsum_tree && e->alone && e->gsum_wave;
+    if (wave)
+      hipLaunchKernelGGL(k_gsum_wave, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>(),
+                         e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
+    else if (e->straus_run)
+      hipLaunchKernelGGL(k_gsum_straus, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
+                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(), live,
+                         e->pk3.as<uint32_t>(), e->scalars.as<uint64_t>(), e->gacc.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu,
+                         e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
+                         e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
     // the per-root tree over the chunk sums (levels until one partial per root is left)
-    const bool tree = e->gsum_tree && e->gchunk == LB_GROUP_CHUNK_ALONE;
+    const bool tree = e->gsum_tree && e->alone && !wave;  // (the Straus chunks under load are 8 members too)
     for (uint32_t st = 1; tree && st < e->gmax_chunks; st *= LB_GSUM_FAN)
       hipLaunchKernelGGL(k_gsum_tree, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->chunk_root.as<uint32_t>(), st, e->gacc.as<uint32_t>());
     hipLaunchKernelGGL(k_gsum_final, dim3(nblk_inv(nuh)), dim3(LB_INV_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                        e->gacc.as<uint32_t>(), e->gp_aff.as<uint32_t>(), e->gp_inf.as<uint32_t>(),
-                       tree ? 0u : 1u);
+                       wave ? 2u : (tree ? 0u : 1u));
   }
   {
     stage_scope sc(e, ST_MILLER, s1);
@@ -919,12 +987,17 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
 // Runs the batch pipeline on two streams: the job S tree (leaf count mj = pow2 >= jobs) with
 // fS = ML(-G1, S_root) on s2, the message product tree (leaf count mu = pow2 >= sets, leaves
 // [0, n_u) live) on s1, joined on s1 ready for the root check.
-static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu) {
+static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, uint32_t& mj, uint32_t& mu,
+                            bool unblinded) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
   e->partial_serial = 0;
   e->alone = device_alone(e);
-  e->gchunk = (e->alone && e->gsum_tree) ? LB_GROUP_CHUNK_ALONE : LB_GROUP_CHUNK;
-  int st = fill_scalars(e, n, scalars);
+  e->straus_run = e->straus && !e->alone;
+  e->rpk_stale = e->straus_run;
+  e->gchunk = (e->alone && e->gsum_tree) ? (e->gsum_wave ? LB_GROUP_CHUNK_WAVE : LB_GROUP_CHUNK_ALONE)
+                                          : (e->straus_run ? LB_STRAUS_CHUNK : LB_GROUP_CHUNK);
+  const bool one_unblinded = n == 1 && !scalars && unblinded;
+  int st = fill_scalars(e, n, scalars, unblinded);
   if (st != LB_OK) return st;
   mj = 1;
   while (mj < nj) mj <<= 1;
@@ -1009,10 +1082,15 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     const bool pk_split = s3 != s2;
     {
       stage_scope sc(e, ST_PK_BLIND, s3);
-      for (uint32_t mode = pk_split ? 1u : 0u; mode <= (pk_split ? 2u : 0u); mode++) {
+      // modes: 0 all, 1 aggregate + status (+ pk3 for the Straus sums), 2 the per-set ladder
+      const uint32_t m0 = (pk_split || e->straus_run) ? 1u : 0u;
+      const uint32_t m1 = e->straus_run ? 1u : (pk_split ? 2u : 0u);
+      if (e->straus_run) LB_HIP(e->pk3.ensure((size_t)ns * sizeof(g1x3)));
+      for (uint32_t mode = m0; mode <= m1; mode++) {
         hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s3, n, nc, b->d_set_chunk_off.as<uint32_t>(),
                            e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
-                           e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>(), mode);
+                           e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>(), mode,
+                           (mode == 1u && e->straus_run) ? e->pk3.as<uint32_t>() : nullptr);
         if (mode == 1u) LB_HIP(hipEventRecord(e->ev_pkst, s3));
       }
     }
@@ -1123,7 +1201,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       }
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
-    if (n == 1 && !scalars) {
+    if (one_unblinded) {
       stage_scope sc(e, ST_SIG_MSM, s2);
       hipLaunchKernelGGL(k_sig_unblinded, dim3(1), dim3(64), 0, s2, e->sig_aff.as<uint32_t>(),
                          e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), 2 * mj, e->treeS.as<uint32_t>());
@@ -1613,6 +1691,15 @@ static int32_t search_root_sums(lb_engine* e, const search_ctx& x) {
 
 static int32_t search_invalid(lb_engine* e, lb_batch* b, uint32_t mu, int32_t* out_job) {
   const uint32_t n = b->n_sets, nj = b->n_jobs;
+  if (e->rpk_stale && n) {
+    // the per-root sums ran the Straus form (no per-set r PK): the search's range sums need them
+    hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, e->stream, n, b->n_chunks,
+                       b->d_set_chunk_off.as<uint32_t>(), e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(),
+                       e->pk_aff.as<uint32_t>(), e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(),
+                       e->pk_status.as<int32_t>(), 2u, nullptr);
+    LB_HIP(hipGetLastError());
+    e->rpk_stale = false;
+  }
   search_ctx x;
   x.n = n;
   x.mu = mu;
@@ -1839,7 +1926,7 @@ static int32_t verify_locked(lb_engine* e, lb_batch* b, const uint64_t* scalars,
   if (nj == 0) return LB_OK;
   uint32_t m = 1, mu = 1;
   busy_scope busy(e->device, e, e->latency);
-  int32_t st = run_pipeline(e, b, scalars, m, mu);
+  int32_t st = run_pipeline(e, b, scalars, m, mu, true);
   if (st != LB_OK) return st;
   // root verdict on s1 (after the join)
   LB_HIP(e->verdict.ensure(4));
@@ -1886,7 +1973,7 @@ extern "C" int32_t lb_batch_partial(lb_engine* e, lb_batch* b, const uint64_t* s
     return LB_OK;
   }
   busy_scope busy(e->device, e, e->latency);
-  int32_t st = run_pipeline(e, b, scalars, m, mu);
+  int32_t st = run_pipeline(e, b, scalars, m, mu, false);  // always blinded: multiplied with other partials
   if (st != LB_OK) return st;
   LB_HIP(e->parts.ensure(576));
   {

@@ -357,19 +357,20 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_subgroup_row(uint32_t n, const u
   r_run(S, &LBR_OPS_XLADDER, LBR_OPS_XLADDER.n);
   if (r_zero_mask(S, 2, [&](int e) { return X + 4 + e; }) == 3) r_g2_mul_xabs<false>(S, X, P);
   r_g2_psi(S, PSI, P);
-  r_export(S, X, 12);
-  if (r_tid() == 0) {
-    g2j acc, ps;
-    acc.x = fp2{r_fp_of_staged(S, 0), r_fp_of_staged(S, 1)};
-    acc.y = fp2{r_fp_of_staged(S, 2), r_fp_of_staged(S, 3)};
-    acc.z = fp2{r_fp_of_staged(S, 4), r_fp_of_staged(S, 5)};
-    ps.x = fp2{r_fp_of_staged(S, 6), r_fp_of_staged(S, 7)};
-    ps.y = fp2{r_fp_of_staged(S, 8), r_fp_of_staged(S, 9)};
-    ps.z = fp2{r_fp_of_staged(S, 10), r_fp_of_staged(S, 11)};
-    bool ok = !jac_is_inf(acc);  // psi(P) is finite
-    if (ok) ok = jac_eq(ps, jac_neg(acc));
-    if (!ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
-  }
+  // psi(P) == -acc on the row, from G2ADD's exceptional-case values (round 6: the lane-0 jac_eq
+  // epilogue cost the kernel 1.5 KB of private segment per lane at the 1 024-thread workgroup's
+  // 128 VGPRs): with both points finite, H = 0 <=> equal x, and then r = 0 <=> equal y, so
+  // psi(P) = -acc <=> H = 0 and (r != 0 or y(acc) = 0).  Bits: 0-1 Z of psi(P), 2-3 Z of acc,
+  // 4-5 H, 6-7 r, 8-9 y of acc (r_zero_mask tests canonical values: exact)
+  r_gather(S, LBR_IN, 12, [&](int e) { return e < 6 ? PSI + e : X + e - 6; });
+  r_exec(S, LBR_G2ADD);
+  const lds_i32* prog = r_progs(S) + LBR_G2ADD;
+  const uint32_t m = r_zero_mask(S, 10, [&](int e) {
+    return e < 2 ? PSI + 4 + e : (e < 4 ? X + 2 + e : (e < 8 ? prog[4 + e] : X + 2 + (e - 8)));
+  });
+  const bool ok = (m & 0x3) != 0x3 && (m & 0xc) != 0xc && (m & 0x30) == 0x30 &&
+                  ((m & 0xc0) != 0xc0 || (m & 0x300) == 0x300);
+  if (r_tid() == 0 && !ok) sig_status[i] = LB_POINT_NOT_IN_GROUP;
 }
 #endif  // LB_KG
 
@@ -849,23 +850,66 @@ __global__ void __launch_bounds__(LBR_NT) k_hash_finish_row(uint32_t n, const ui
 // keys so a 512-key sync aggregate costs one chunk's latency plus a short combine instead of
 // 512 serial additions on one lane; chunk c covers pubkeys [chunk_lo[c], chunk_lo[c+1]) of one set.
 #define LB_PK_CHUNK 16
+// chunk_lo[c] bit 31: chunk c is its set's first (lb_engine.hip batch_fill; the sentinel
+// chunk_lo[nc] carries it too)
+#define LB_CHUNK_FIRST 0x80000000u
+#define LB_CHUNK_LO(v) ((v) & 0x7fffffffu)
+
+// Round 6: the chunk sums of one set are combined by a segmented shuffle tree over the wave (64
+// chunks per wave, one workgroup = one wave) instead of serially on one lane in k_pk_blind: lane
+// t's segment is the run of lanes of its set inside the wave (heads from the LB_CHUNK_FIRST flags
+// by ballot), and after log2(64) levels the segment's first lane holds the segment's sum.  A set's
+// sum is then the sum of its segment heads: its first chunk and every later chunk at a wave
+// boundary (c % 64 == 0), at most 1 + ceil(chunks / 64) of them (k_pk_blind).  The same for the
+// per-root sums of a batch alone (k_gsum_wave).  (north_star: tree reduction for G1 aggregation.)
+__device__ __forceinline__ g1j g1j_shfl_down(const g1j& a, unsigned d) {
+  return g1j{fp_shfl_down(a.x, d), fp_shfl_down(a.y, d), fp_shfl_down(a.z, d)};
+}
+// v: this lane's partial; rel: lanes of its segment before it; left: lanes of its segment from it on
+template <class F>
+__device__ __forceinline__ jac<F> wave_seg_sum(jac<F> v, uint32_t rel, uint32_t left) {
+  LB_UNROLL for (uint32_t s = 1; s < 64; s <<= 1) {
+    const jac<F> o = jac_as<F>(g1j_shfl_down(jac_as<fp>(v), s));
+    if ((rel & (2 * s - 1)) == 0 && s < left) v = jac_add_i<F, true>(v, o);
+  }
+  return v;
+}
+// segments of the wave from per-lane "starts a segment" flags (inactive lanes: pass true)
+__device__ __forceinline__ void wave_segments(bool starts, uint32_t& rel, uint32_t& left) {
+  const uint64_t heads = __ballot(starts) | 1ull;  // the wave's first lane always starts one
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  const uint32_t hl = 63 - __clzll(heads & upto);
+  const uint64_t after = heads & ~upto;
+  const uint32_t el = after ? (uint32_t)__ffsll((long long)after) - 1 : 64;
+  rel = lane - hl;
+  left = el - lane;
+}
 #if LB_KG(4)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, const uint32_t* __restrict__ chunk_lo,
                                                       const uint8_t* __restrict__ pks, uint32_t* __restrict__ chunk_acc,
                                                       int32_t* __restrict__ chunk_status) {
   uint32_t c = lb_tid();
-  if (c >= nc) return;
-  uint32_t a = chunk_lo[c], e = chunk_lo[c + 1];
+  if (blockIdx.x * LB_TPB >= nc) return;  // whole wave idle (uniform)
+  const bool act = c < nc;
+  const uint32_t cl = act ? chunk_lo[c] : LB_CHUNK_FIRST;
   int st = LB_OK;
   g1j acc = jac_infinity<fp>();
-  for (uint32_t k = a; k < e && st == LB_OK; k++) {
-    uint8_t b[96];
-    ld_bytes<96>(b, pks + (size_t)96 * k);
-    g1a p;
-    bool inf;
-    st = g1_deserialize96(b, p, inf);
-    if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+  if (act) {
+    const uint32_t a = LB_CHUNK_LO(cl), e = LB_CHUNK_LO(chunk_lo[c + 1]);
+    for (uint32_t k = a; k < e && st == LB_OK; k++) {
+      uint8_t b[96];
+      ld_bytes<96>(b, pks + (size_t)96 * k);
+      g1a p;
+      bool inf;
+      st = g1_deserialize96(b, p, inf);
+      if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+    }
   }
+  uint32_t rel, left;
+  wave_segments((cl & LB_CHUNK_FIRST) != 0, rel, left);
+  acc = wave_seg_sum(acc, rel, left);
+  if (!act) return;
   soa_st(chunk_acc, nc, c, acc);
   chunk_status[c] = st;
 }
@@ -876,6 +920,10 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_chunks(uint32_t nc, cons
 // << 1) | is_infinity.  A gather by validator index touches one L2 line (a word-major layout
 // touched 24 lines + 1 for the flag: with a mainnet-sized table every one a miss).
 #define LB_TABLE_REC 32
+// an affine G1 point with beta x (the GLV endomorphism [lambda]P = (beta x, y)): 144 B, AoS
+struct g1x3 {
+  fp x, y, bx;
+};
 __device__ __forceinline__ g1a table_ld(const uint32_t* __restrict__ table, uint32_t t) {
   return aos_ld<g1a>(table + (size_t)LB_TABLE_REC * t, 0);
 }
@@ -891,24 +939,32 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_G1) k_pk_chunks_idx(uint32_t n
                                                           uint32_t* __restrict__ chunk_acc,
                                                           int32_t* __restrict__ chunk_status) {
   uint32_t c = lb_tid();
-  if (c >= nc) return;
-  uint32_t a = chunk_lo[c], e = chunk_lo[c + 1];
+  if (blockIdx.x * LB_TPB >= nc) return;  // whole wave idle (uniform)
+  const bool act = c < nc;
+  const uint32_t cl = act ? chunk_lo[c] : LB_CHUNK_FIRST;
   int st = LB_OK;
   jac<lb_g1f> acc = jac_infinity<lb_g1f>();
-  for (uint32_t k = a; k < e; k++) {
-    uint32_t t = idx[k];
-    if (t >= table_n) {
-      st = LB_ERR_ARGUMENT;
-      break;
+  if (act) {
+    const uint32_t a = LB_CHUNK_LO(cl), e = LB_CHUNK_LO(chunk_lo[c + 1]);
+    for (uint32_t k = a; k < e; k++) {
+      uint32_t t = idx[k];
+      if (t >= table_n) {
+        st = LB_ERR_ARGUMENT;
+        break;
+      }
+      const uint32_t fl = table_flag_ld(table, t);
+      if (fl >> 1) {
+        st = (int)(fl >> 1);
+        break;
+      }
+      if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
+      acc = jac_add_aff_i<lb_g1f, true>(acc, aff_as<lb_g1f>(table_ld(table, t)));
     }
-    const uint32_t fl = table_flag_ld(table, t);
-    if (fl >> 1) {
-      st = (int)(fl >> 1);
-      break;
-    }
-    if (fl & 1u) continue;  // infinity contributes nothing to the aggregate
-    acc = jac_add_aff_i<lb_g1f, true>(acc, aff_as<lb_g1f>(table_ld(table, t)));
   }
+  uint32_t rel, left;
+  wave_segments((cl & LB_CHUNK_FIRST) != 0, rel, left);
+  acc = wave_seg_sum(acc, rel, left);
+  if (!act) return;
   soa_st(chunk_acc, nc, c, jac_as<fp>(acc));
   chunk_status[c] = st;
 }
@@ -963,9 +1019,12 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
                                                          uint32_t* __restrict__ pk_aff,
                                                          const uint64_t* __restrict__ scalars,
                                                          uint32_t* __restrict__ rpk,
-                                                         int32_t* __restrict__ pk_status, uint32_t mode) {
+                                                         int32_t* __restrict__ pk_status, uint32_t mode,
+                                                         uint32_t* __restrict__ pk3) {
   // mode 0: all; 1: the aggregate, its status and affine form only (pk_status, pk_aff: what the
-  // job statuses need, ahead of the ladder); 2: the ladder only, from mode 1's pk_status / pk_aff
+  // job statuses need, ahead of the ladder); 2: the ladder only, from mode 1's pk_status / pk_aff.
+  // pk3 (mode 1, optional): (x, y, beta x) per set, AoS, for the per-root Straus sums
+  // (k_gsum_straus), which then replace the ladder
   const uint32_t i = blockIdx.x * LB_INV_TPB + threadIdx.x;
   const bool act = i < n;
   int st = LB_ERR_ARGUMENT;
@@ -993,9 +1052,12 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
     uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
     st = (c0 == c1) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
     g1j acc = jac_infinity<fp>();
+    // every chunk's status, the segment heads' sums (k_pk_chunks[_idx]: the set's first chunk and
+    // its chunks at wave boundaries)
     for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
       st = chunk_status[c];
-      if (st == LB_OK) acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add_i<fp, true>(acc, soa_ld<g1j>(chunk_acc, nc, c));
+      if (st == LB_OK && (c == c0 || (c & (LB_TPB - 1)) == 0))
+        acc = (c == c0) ? soa_ld<g1j>(chunk_acc, nc, c) : jac_add_i<fp, true>(acc, soa_ld<g1j>(chunk_acc, nc, c));
     }
     if (st == LB_OK && jac_is_inf(acc)) st = LB_PK_IS_INFINITY;
     rj = acc;
@@ -1018,6 +1080,7 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
   if (mode == 1) {  // uniform
     if (!act) return;
     if (ok) soa_st(pk_aff, n, i, pk);
+    if (pk3 != nullptr) aos_st(pk3, i, g1x3{pk.x, pk.y, ok ? fp_mul(pk.x, fp_load(LB_GLV_BETA)) : fp_zero()});
     pk_status[i] = st;
     return;
   }
@@ -1231,6 +1294,9 @@ __global__ void __launch_bounds__(64) k_miller_wave(uint32_t n, uint32_t m, cons
 #define LB_GROUP_CHUNK_ALONE 8
 #endif
 #define LB_GROUP_CHUNK 32
+#ifndef LB_GROUP_CHUNK_WAVE
+#define LB_GROUP_CHUNK_WAVE 4  // ... with k_gsum_wave's shuffle tree (64 chunks of a wave: 256 members)
+#endif
 #ifndef LB_GSUM_FAN
 #define LB_GSUM_FAN 4     // partial sums combined per lane and level in k_gsum_tree
 #endif
@@ -2533,6 +2599,100 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
 }
 #endif  // LB_KG
 
+// Chunk c of a group (<= LB_STRAUS_CHUNK members of one root): sum over its live members of
+// r_i PK_i with the blinding folded in (round 6, the loaded-device form): r_i = lo_i + hi_i lambda,
+// so the chunk sum is a joint (Straus) double-and-add over the 32 bit positions of all its
+// members' lo / hi halves, ONE doubling chain per chunk instead of one per set:
+//   acc = 2 acc;  acc += T_k[d_k]  for each member k with digit d_k = lo_k bit + 2 hi_k bit,
+//   T_k = {PK, [lambda]PK = (beta x, y), PK + [lambda]PK = (beta^2 x, -y) = (-x - beta x, -y)}.
+// Per set ~32 mixed additions + 32/8 doublings against k_pk_blind's per-set ladder (32 + 32) and
+// the chunk sum's Jacobian addition.  Equal keys in a chunk (duplicate validators) meet P = +-Q:
+// jac_add_aff_i handles them.  The per-set r_i PK_i (the search's) come from k_pk_blind mode 2
+// when a search needs them.
+#ifndef LB_STRAUS_CHUNK
+#define LB_STRAUS_CHUNK 8
+#endif
+#if LB_KG(14)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_straus(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                        const uint32_t* __restrict__ gch,
+                                                        const uint32_t* __restrict__ chunk_beg,
+                                                        const uint32_t* __restrict__ chunk_end,
+                                                        const uint32_t* __restrict__ members,
+                                                        const uint32_t* __restrict__ set_live,
+                                                        const uint32_t* __restrict__ pk3,
+                                                        const uint64_t* __restrict__ scalars,
+                                                        uint32_t* __restrict__ gacc) {
+  const uint32_t c = lb_tid();
+  if (c >= gch[*n_u]) return;
+  const uint32_t b = chunk_beg[c], m = chunk_end[c] - b;
+  uint32_t idx[LB_STRAUS_CHUNK], lo[LB_STRAUS_CHUNK], hi[LB_STRAUS_CHUNK];
+  LB_UNROLL for (int k = 0; k < LB_STRAUS_CHUNK; k++) {
+    idx[k] = 0;
+    lo[k] = hi[k] = 0;  // absent or dead members: digit 0 throughout
+    if ((uint32_t)k < m) {
+      const uint32_t i = members[b + k];
+      idx[k] = i;
+      if (set_live[i]) {
+        const uint64_t w = scalars[i];
+        lo[k] = (uint32_t)w;
+        hi[k] = (uint32_t)(w >> 32);
+      }
+    }
+  }
+  jac<lb_g1f> acc = jac_infinity<lb_g1f>();
+#pragma clang loop unroll(disable)
+  for (int bit = 31; bit >= 0; bit--) {
+    if (!jac_is_inf(acc)) acc = jac_dbl_i(acc);
+    LB_UNROLL for (int k = 0; k < LB_STRAUS_CHUNK; k++) {
+      const uint32_t d = ((lo[k] >> bit) & 1u) | (((hi[k] >> bit) & 1u) << 1);
+      if (d != 0u) {
+        const g1x3 t = aos_ld<g1x3>(pk3, idx[k]);
+        aff<lb_g1f> q;
+        q.x = lb_g1f{d == 1u ? t.x : (d == 2u ? t.bx : fp_neg(fp_add(t.x, t.bx)))};
+        q.y = lb_g1f{d == 3u ? fp_neg(t.y) : t.y};
+        acc = jac_add_aff_i<lb_g1f, true>(acc, q);
+      }
+    }
+  }
+  soa_st(gacc, n, c, jac_as<fp>(acc));
+}
+#endif  // LB_KG
+
+// Per-root sums of a batch alone (round 6; replaces k_gsum_chunks + the k_gsum_tree launches):
+// the chunk sums of r_i PK_i (<= gchunk members per lane), then a segmented shuffle tree over the
+// wave's 64 chunks by root (wave_seg_sum); the first lane of each (root, wave) segment writes the
+// segment's sum to gacc, and k_gsum_final (mode 2) adds a root's segment heads.  One launch, the
+// partials in registers, log2(64) levels.
+#if LB_KG(14)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_wave(uint32_t n, const uint32_t* __restrict__ n_u,
+                                                      const uint32_t* __restrict__ gch,
+                                                      const uint32_t* __restrict__ chunk_beg,
+                                                      const uint32_t* __restrict__ chunk_end,
+                                                      const uint32_t* __restrict__ chunk_root,
+                                                      const uint32_t* __restrict__ members,
+                                                      const uint32_t* __restrict__ set_live,
+                                                      const uint32_t* __restrict__ rpk,
+                                                      uint32_t* __restrict__ gacc) {
+  const uint32_t c = lb_tid(), nch = gch[*n_u];
+  if (blockIdx.x * LB_TPB >= nch) return;  // whole wave idle (uniform)
+  const bool act = c < nch;
+  jac<lb_g1f> acc = jac_infinity<lb_g1f>();
+  bool starts = true;
+  if (act) {
+    for (uint32_t k = chunk_beg[c]; k < chunk_end[c]; k++) {
+      const uint32_t i = members[k];
+      if (!set_live[i]) continue;
+      acc = jac_add_i<lb_g1f, true>(acc, jac_as<lb_g1f>(aos_ld<g1j>(rpk, i)));
+    }
+    starts = c == gch[chunk_root[c]];
+  }
+  uint32_t rel, left;
+  wave_segments(starts, rel, left);
+  acc = wave_seg_sum(acc, rel, left);
+  if (act && rel == 0) soa_st(gacc, n, c, jac_as<fp>(acc));
+}
+#endif  // LB_KG
+
 // One level of the per-root sum tree over the chunk sums (in place, strided): at stride s, the
 // lane of chunk c with (c - gch[u]) a multiple of LB_GSUM_FAN s adds the partials at c + k s,
 // k = 1 .. LB_GSUM_FAN - 1, of its own root; after the levels with s < max chunks per root,
@@ -2569,9 +2729,11 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW) k_gsum_final(uint32_t n, 
   const bool act = u < nu;
   g1j acc = jac_infinity<fp>();
   if (act) {
-    if (serial)  // (A/B: LB_GSUM_TREE=0) the root's chunk sums added on this lane
+    if (serial == 1)  // (under load, and A/B: LB_GSUM_TREE=0) the root's chunk sums added on this lane
       for (uint32_t c = gch[u]; c < gch[u + 1]; c++) acc = jac_add(acc, soa_ld<g1j>(gacc, n, c));
-    else
+    else if (serial == 2)  // k_gsum_wave: the root's segment heads (first chunk, then wave boundaries)
+      for (uint32_t c = gch[u]; c < gch[u + 1]; c = (c / LB_TPB + 1) * LB_TPB) acc = jac_add(acc, soa_ld<g1j>(gacc, n, c));
+    else  // k_gsum_tree: the tree's root
       acc = soa_ld<g1j>(gacc, n, gch[u]);
   }
   const bool zero = jac_is_inf(acc);

@@ -190,6 +190,11 @@ class Engine:
     def __exit__(self, *a):
         self.close()
 
+    @property
+    def cu_count(self) -> int:
+        """CUs this engine's streams may use (lb_engine_cu_count)."""
+        return int(self.lib.lb_engine_cu_count(self.h))
+
     # ---------------------------------------------------------------- verification
     def upload(self, jobs_or_packed) -> Batch:
         packed = jobs_or_packed if isinstance(jobs_or_packed, PackedJobs) else pack_jobs(jobs_or_packed)

@@ -6,7 +6,10 @@
  *   - a call is split into jobs of >= 128 sets (chunkifyMaximizeChunkSize, multithread/utils.ts:4-19);
  *   - batchable jobs are buffered until > 32 sigs or 100 ms (:48, :57, :257-275);
  *   - non-batchable jobs run on the next tick (:280-283);
- *   - verifyOnMainThread verifies synchronously on the caller's thread (:138-151);
+ *   - verifyOnMainThread goes straight to its own latency engine, past the buffer and the queue
+ *     (:138-151); the reference runs it synchronously and blocks the event loop for the whole
+ *     verification, here only the marshalling runs on the loop and the Promise<boolean> settles
+ *     when the device is done (the contract is the same Promise);
  *   - each job resolves true / false or rejects with the blst error string, independently of the
  *     other jobs in the same GPU batch (multithread.test.ts:86-103);
  *   - close() rejects queued jobs with QUEUE_ABORTED (:176-197).
@@ -30,8 +33,8 @@
  * Malformed inputs (root not 32 bytes, pubkey of another length, signature not a Uint8Array)
  * reject only the call that carries them, before anything is queued.
  *
- * Synchronous entry points (verifyOnMainThread, verifySignatureSet, aggregateSignatures, key
- * decompression) run on their own engine, outside the async pool, so a main-thread call never
+ * Main-thread entry points (verifyOnMainThread, and the synchronous verifySignatureSet,
+ * aggregateSignatures, key decompression) run on their own engine, outside the async pool, so a main-thread call never
  * waits behind a gossip batch holding a pool engine (the reference runs them on the main thread
  * while workers are busy, multithread/index.ts:138-151).
  */
@@ -277,7 +280,22 @@ class BlsGpuVerifier {
     return keys.map((k, i) => new GpuPublicKey(first + i, flat.subarray(96 * i, 96 * i + 96)));
   }
 
-  /** one job verified synchronously on the caller's thread (the reference's main-thread path) */
+  /**
+   * The reference's main-thread path (multithread/index.ts:138-151) without blocking the event
+   * loop: one job on the latency engine through the addon's engine thread.  Malformed input
+   * rejects the returned promise (the reference throws from the same call).
+   */
+  verifyMainThread(sets) {
+    const t0 = Date.now();
+    return addon.verifyJobs(this.syncEngine, ...packJobs([normalizeSets(sets, this.decompress)])).then((res) => {
+      const dt = Date.now() - t0;
+      this.stats.mainThreadMs += dt;
+      if (this.metrics) this.metrics.blsThreadPool.mainThreadDurationInThreadPool.observe(dt / 1000);
+      return codeToResult(res[0]);
+    });
+  }
+
+  /** one job verified synchronously on the caller's thread (state-transition verifySignatureSet) */
   verifySync(sets) {
     const t0 = Date.now();
     const res = addon.verifyJobsSync(this.syncEngine, ...packJobs([normalizeSets(sets, this.decompress)]));
@@ -329,7 +347,7 @@ class BlsGpuVerifier {
     try {
       if (this.closed) throw new QueueError({code: QueueErrorCode.QUEUE_ABORTED});
       if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(getAggregatedPubkeysCount(sets));
-      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) return Promise.resolve(this.verifySync(sets));
+      if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) return this.verifyMainThread(sets);
       sets = normalizeSets(sets, this.decompress);
     } catch (e) {
       return Promise.reject(e);

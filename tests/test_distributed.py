@@ -245,3 +245,132 @@ def test_search_after_partial_rejects_a_successor_batch():
             assert np.array_equal(b2.search_after_partial(), w2.expected)
         finally:
             b2.free()
+
+
+def _cancel_jobs():
+    from lodestar_amd.engine import SetInput
+    c = load_json("cancel_pair.json")["sets"]
+    return [[SetInput([bytes.fromhex(s["pubkey"])], bytes.fromhex(s["signing_root"]),
+                      bytes.fromhex(s["signature"]))] for s in c]
+
+
+def test_cancel_pair_fixture_cancels_only_unblinded():
+    """The fixture is a real attack on unblinded 1-set partials: each set alone is invalid, the
+    product with r_A = r_B = 1 is one, random blinding rejects it (oracle, pure Python)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import bls_oracle as O
+    c = load_json("cancel_pair.json")["sets"]
+    pk = [O.g1_deserialize(bytes.fromhex(s["pubkey"])) for s in c]
+    m = [bytes.fromhex(s["signing_root"]) for s in c]
+    sg = [O.g2_decompress(bytes.fromhex(s["signature"])) for s in c]
+    assert [O.core_verify(pk[i], m[i], sg[i]) for i in range(2)] == [False, False]
+    assert O.verify_multiple_signatures(list(zip(pk, m, sg)), scalars=[1, 1])
+    assert not O.verify_multiple_signatures(list(zip(pk, m, sg)), scalars=[3, 5])
+
+
+@pytest.mark.gpu
+def test_single_set_partials_are_blinded():
+    """Round-5 ADVICE: lb_batch_partial of a 1-set batch must not be unblinded, or two ranks'
+    shards sig_A + D and sig_B - D cancel in lb_fp12_product_is_one.  Each 1-set batch's
+    lb_batch_verify stays false (the unblinded single-set path), and the product of the two
+    partials is not one."""
+    from lodestar_amd.engine import Engine
+    jobs = _cancel_jobs()
+    with Engine(0) as eng:
+        parts = []
+        for j in jobs:
+            b = eng.upload([j])
+            try:
+                assert list(b.verify()) == [0]
+                f, st = b.partial()
+                assert list(st) == [1]
+                parts.append(f)
+            finally:
+                b.free()
+        assert not eng.product_is_one(parts)
+        assert not eng.product_is_one(parts[::-1])
+
+
+def _worker_cancel(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from lodestar_amd.distributed import verify_sharded
+    from lodestar_amd.engine import Engine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        b = eng.upload([_cancel_jobs()[rank]])   # one single-set shard per rank
+        try:
+            codes, ok = verify_sharded(b.partial, eng.product_is_one, b.search_after_partial)
+        finally:
+            b.free()
+        out.put((rank, codes, ok))
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_single_set_shards_cannot_cancel():
+    """Two ranks, one single-set shard each, with opposite offsets on the two signatures: the
+    exchange must reject the segment and each rank must report its job invalid."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_cancel, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, [0], False), (1, [0], False)]
+
+
+def _worker_nccl(port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from lodestar_amd import workloads as W
+    from lodestar_amd.distributed import verify_sharded
+    from lodestar_amd.engine import Engine
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    res = {"backend": dist.get_backend()}
+    eng = Engine(0)
+    try:
+        for name in ("c5", "c4"):   # a valid shard, then one with planted wrong / malformed sets
+            wl = W.make(eng, name)
+            b = eng.upload(W.indexed_for(eng, wl))
+            try:
+                codes, ok = verify_sharded(b.partial, eng.product_is_one, b.search_after_partial,
+                                           device=torch.device("cuda", 0))
+            finally:
+                b.free()
+            res[name] = (codes == [int(x) for x in wl.expected], ok)
+        out.put(res)
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_nccl_world_one_exchange_on_device():
+    """RCCL on hardware: an "nccl" process group of world size 1 on device 0,
+    verify_sharded with the 576-B partial as a device tensor (all_gather over RCCL), then
+    lb_fp12_product_is_one: a valid shard accepts, a shard with planted invalid jobs rejects and
+    the search names them."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_nccl, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res["backend"] == "nccl"
+    assert res["c5"] == (True, True)
+    assert res["c4"] == (True, False)

@@ -752,11 +752,14 @@ def test_row_engine_forms_agree(monkeypatch, name):
     case tests), the Miller loops and tree nodes (LB_ROW_MAX), ML(-G1, S), the root checks and
     partials (LB_ROW_FE).  Against the wave / 8-lane forms (all row forms off) on the same batch
     and blinding scalars: same verdicts, byte-identical root partials (576-byte Fp12 products
-    before the final exponentiation).  c1 (one set) takes the unblinded path (scalar 1)."""
+    before the final exponentiation).  LB_ALONE=1 pins the engine's "device alone" test, so the row
+    forms run whatever other engines did just before (round-5 ADVICE: a recent pipeline exit sent
+    every configuration to the wave forms and the comparison compared nothing different)."""
     from lodestar_amd.engine import Engine
     from lodestar_amd import workloads as W
     outs = []
     big = str(1 << 20)
+    monkeypatch.setenv("LB_ALONE", "1")
     for row_fe, row_max, hash_max, careful in (("1", None, None, "0"), ("0", "0", "0", "0"),
                                                ("1", "64", big, "1")):
         monkeypatch.setenv("LB_ROW_FE", row_fe)
@@ -839,3 +842,72 @@ def test_latency_engine_under_load():
     assert r.returncode == 0
     ms = [float(x) for x in r.stdout.strip().splitlines()[-1].split()]
     assert sorted(ms)[len(ms) // 2] < 8.0, ms
+
+
+@pytest.mark.gpu
+def test_latency_partition_released_with_last_latency_engine():
+    """Round-5 VERDICT item 7 / ADVICE: the CU partition lives while a latency engine does.  A
+    latency engine gets the reserved CUs, a pool engine created beside it the rest; once both are
+    gone, a new pool engine reports the device's full CU count (lb_engine_cu_count)."""
+    import torch
+    from lodestar_amd.engine import Engine
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    with Engine(0) as before:
+        assert before.cu_count == ncu
+    lat = Engine(0, Engine.LATENCY)
+    pool = Engine(0)
+    try:
+        r = lat.cu_count
+        assert 1 <= r <= ncu // 4
+        assert pool.cu_count == ncu - r
+        with Engine(0, Engine.LATENCY) as lat2:   # a second latency engine shares the partition
+            assert lat2.cu_count == r
+    finally:
+        pool.close()
+        lat.close()
+    with Engine(0) as after:
+        assert after.cu_count == ncu
+
+
+@pytest.mark.gpu
+def test_engine_cap_reserves_scratch():
+    """The engine cap's worth of engines (10) each reserve s1, s2 and s3 scratch at creation, then
+    verify at once with no queue abort (child process: the engine count is per process)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gpu_engines_child.py")],
+                       capture_output=True, text=True, timeout=240)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3_mixed", "c4", "c2"])
+def test_per_root_sum_forms_agree(monkeypatch, name):
+    """Round 6 per-root sum forms, each pinned with LB_ALONE: under load (LB_ALONE=0) the Straus
+    chunk sums with the blinding folded in (k_gsum_straus; the per-set r PK computed only for a
+    search) against the per-set ladder + chunk sums (LB_GSUM_STRAUS=0); alone (LB_ALONE=1) the
+    segmented shuffle tree (k_gsum_wave) against the k_gsum_tree launches (LB_GSUM_WAVE=0) and the
+    serial chunk combine (LB_GSUM_TREE=0).  Same verdicts (c4 carries wrong and malformed sets, so
+    its search runs from the Straus form's lazily computed r PK), byte-identical root partials."""
+    from lodestar_amd.engine import Engine
+    from lodestar_amd import workloads as W
+    outs = []
+    for alone, straus, wave, tree in (("0", "1", "1", "1"), ("0", "0", "1", "1"), ("1", "1", "1", "1"),
+                                      ("1", "1", "0", "1"), ("1", "1", "1", "0")):
+        monkeypatch.setenv("LB_ALONE", alone)
+        monkeypatch.setenv("LB_GSUM_STRAUS", straus)
+        monkeypatch.setenv("LB_GSUM_WAVE", wave)
+        monkeypatch.setenv("LB_GSUM_TREE", tree)
+        with Engine(0) as e:
+            wl = W.make(e, name)
+            b = e.upload(W.indexed_for(e, wl))
+            try:
+                sc = np.random.default_rng(9).integers(1, 1 << 63, size=wl.packed.n_sets, dtype=np.uint64)
+                got = np.asarray(b.verify(scalars=sc))[:wl.packed.n_jobs]
+                part = bytes(b.partial(scalars=sc)[0])
+            finally:
+                b.free()
+        assert np.array_equal(got, wl.expected), (alone, straus, wave, tree, np.nonzero(got != wl.expected))
+        outs.append(part)
+    assert all(o == outs[0] for o in outs), [o[:8].hex() for o in outs]

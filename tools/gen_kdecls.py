@@ -31,6 +31,7 @@ GROUPS = {
     2: ["k_hash_map", "k_sk_to_pk", "k_sign", "k_ssz_zero_hashes", "k_merkleize"],
     3: ["k_hash_finish"],
     4: ["k_miller_lane", "k_pk_chunks", "k_pk_chunks_idx", "k_pk_blind", "k_gsum_chunks", "k_gsum_tree", "k_gsum_final"],
+    14: ["k_gsum_straus", "k_gsum_wave"],
     5: ["k_miller_wave", "k_tree_up_U", "k_ml_S", "k_root_check", "k_root_partial", "k_partials_check", "k_search_ml",
         "k_search_fe", "k_search_match", "k_miller_g8", "k_kzg_check"],
     6: ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],
