@@ -191,27 +191,23 @@ def roofline(counts, packed, stage_ms):
     dom = max(per, key=lambda k: per[k]["fp_mul"])
     ach = per[dom]["tmac_s"]
     wall = stage_ms.get("total") or sum(stage_ms.values())
-    traffic = traffic_corr = None
+    traffic = traffic_src = None
     tp = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tp):
         with open(tp) as f:
             t = json.load(f)
         k = t.get("stages", {}).get(dom)
-        if k and k.get("sets_per_launch") == packed.n_sets:
+        if k and k.get("sets_per_launch") == packed.n_sets and "correction" in t:
             traffic = k["bytes_per_launch"]
-            traffic_corr = k.get("bytes_per_launch_corrected")
-            if traffic_corr is None and t.get("calibration", {}).get("fetch_over_known") and "fetch_bytes" in k:
-                traffic_corr = round(k["fetch_bytes"] / t["calibration"]["fetch_over_known"] + k["write_bytes"])
+            traffic_src = t.get("source")
     return {"bound": "valu-int", "kernel": "stage " + dom, "achieved": ach, "peak": peak,
             "unit": "T int32 MAC/s (v_mad_u64_u32)", "frac": round(ach / peak, 4), "traffic": traffic,
-            "traffic_corrected": traffic_corr,
-            "traffic_note": "HBM bytes per launch of the stage's kernels (profiles/traffic.json, rocprofv3 --pmc "
-                            "FETCH_SIZE and WRITE_SIZE in separate passes at this config, 7 in flight): `traffic` = "
-                            "raw FETCH_SIZE + WRITE_SIZE; `traffic_corrected` = FETCH_SIZE / the fetch calibration "
-                            "measured on k_msg_insert's known 16 B/lane reads + WRITE_SIZE (MI355X_MICROARCH.md: "
-                            "FETCH_SIZE counts half of a wide read); the decode stage's algorithmic bytes are ~700 B "
-                            "per set: 96 B read and 2 x 192 B + status written by the decompression, 192 B re-read "
-                            "by the subgroup check (DESIGN.md 5.2)",
+            "traffic_note": "HBM bytes per launch of the stage's kernels (profiles/traffic.json: rocprofv3 --pmc "
+                            "FETCH_SIZE and WRITE_SIZE in separate passes at this config, 7 in flight), corrected as "
+                            "MI355X_MICROARCH.md prescribes for gfx950: 2 x FETCH_SIZE + WRITE_SIZE; the decode "
+                            "stage's algorithmic bytes are ~700 B per set: 96 B read and 2 x 192 B + status written "
+                            "by the decompression, 192 B re-read by the subgroup check (DESIGN.md 5.2)",
+            "traffic_source": traffic_src,
             "algorithmic_bytes": 700 * packed.n_sets if dom == "decode_sigs" else None,
             "whole_pipeline_frac": round(sum(work.values()) * mac / (wall * 1e-3) / 1e12 / peak, 4),
             "device_ms": round(wall, 3), "stages": per}

@@ -154,7 +154,7 @@ struct lb_engine {
   // a batch alone: the per-root sums' chunks combined by a segmented shuffle tree in one launch
   // (k_gsum_wave, chunks of LB_GROUP_CHUNK_WAVE) instead of the k_gsum_tree launches; LB_GSUM_WAVE=0
   bool gsum_wave = true;
-  dbuf pk3;
+  dbuf pk3, corder;  // (x, y, beta x) per set; the Straus lanes' chunk order (+ size counts)
   bool gsum_tree = true;     // LB_GSUM_TREE=0: the chunk sums added serially per root (A/B)
   // this pipeline run's forms: `alone` (device_alone at its start) picks the latency forms -- the
   // row engine (row_fe: LB_ROW_FE=0 disables it) and the per-root sum tree over 8-member chunks
@@ -584,7 +584,7 @@ void lb_engine_destroy(lb_engine* e) {
                   &e->gch, &e->chunk_beg, &e->chunk_end, &e->members, &e->set_live, &e->gacc, &e->gp_aff,
                   &e->gp_inf, &e->chunk_root, &e->sig_aos, &e->bcnt, &e->bcursor, &e->boff, &e->bch, &e->bchunk_beg,
                   &e->bchunk_end, &e->bmembers, &e->bacc, &e->bsum, &e->wsum, &e->park, &e->set_spec, &e->live_flag, &e->pk_aff, &e->y_root, &e->kzg_g1,
-                  &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set};
+                  &e->kzg_g2, &e->s_terms, &e->s_part, &e->s_root, &e->rs_idx, &e->s_set, &e->pk3, &e->corder};
   for (dbuf* b : bufs) b->release();
   for (dbuf& b : e->sx) b.release();
   for (int i = 0; i < kStages; i++) {
@@ -928,10 +928,20 @@ static hipError_t per_root_chain(lb_engine* e, uint32_t n, uint32_t nuh, uint32_
       hipLaunchKernelGGL(k_gsum_wave, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
                          e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->chunk_root.as<uint32_t>(),
                          e->members.as<uint32_t>(), live, e->rpk.as<uint32_t>(), e->gacc.as<uint32_t>());
-    else if (e->straus_run)
+    else if (e->straus_run) {
+      hipError_t r = e->corder.ensure((size_t)(nch + 2 * (LB_STRAUS_CHUNK + 1)) * 4);
+      if (r != hipSuccess) return r;
+      uint32_t* cnt = e->corder.as<uint32_t>() + nch;
+      r = hipMemsetAsync(cnt, 0, (size_t)2 * (LB_STRAUS_CHUNK + 1) * 4, s1);
+      if (r != hipSuccess) return r;
+      for (uint32_t pass = 0; pass < 2; pass++)
+        hipLaunchKernelGGL(k_chunk_order, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, nu, e->gch.as<uint32_t>(),
+                           e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), cnt, e->corder.as<uint32_t>(), pass);
       hipLaunchKernelGGL(k_gsum_straus, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu, e->gch.as<uint32_t>(),
-                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->members.as<uint32_t>(), live,
-                         e->pk3.as<uint32_t>(), e->scalars.as<uint64_t>(), e->gacc.as<uint32_t>());
+                         e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(), e->corder.as<uint32_t>(),
+                         e->members.as<uint32_t>(), live, e->pk3.as<uint32_t>(), e->scalars.as<uint64_t>(),
+                         e->gacc.as<uint32_t>());
+    }
     else
       hipLaunchKernelGGL(k_gsum_chunks, dim3(nblk(nch)), dim3(LB_TPB), 0, s1, n, nu,
                          e->gch.as<uint32_t>(), e->chunk_beg.as<uint32_t>(), e->chunk_end.as<uint32_t>(),
@@ -2084,28 +2094,44 @@ extern "C" int32_t lb_aggregate_pubkeys(lb_engine* e, uint32_t n_sets, const uin
   uint32_t n_pks = set_pk_offsets[n_sets];
   if (n_pks && !pubkeys) return LB_ERR_ARGUMENT;
   if (!n_sets) return LB_OK;
+  if (n_pks & LB_CHUNK_FIRST) return LB_ERR_ARGUMENT;
   std::lock_guard<std::mutex> lk(e->mu);
   LB_HIP(hipSetDevice(e->device));
-  dbuf off, pk, out, stat;
-  hipError_t r = off.ensure((size_t)(n_sets + 1) * 4);
+  // the batch pipeline's chunk decomposition (<= LB_PK_CHUNK keys, flagged set starts): chunk sums
+  // combined by the wave tree in k_pk_chunks, then k_pk_out96 per set
+  std::vector<uint32_t> sco(n_sets + 1), clo;
+  for (uint32_t i = 0; i < n_sets; i++) {
+    sco[i] = (uint32_t)clo.size();
+    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK)
+      clo.push_back(k | (k == set_pk_offsets[i] ? LB_CHUNK_FIRST : 0u));
+  }
+  sco[n_sets] = (uint32_t)clo.size();
+  const uint32_t nc = (uint32_t)clo.size();
+  clo.push_back(n_pks | LB_CHUNK_FIRST);
+  dbuf dsco, dclo, pk, acc, cst, out, stat;
+  hipError_t r = dsco.ensure(sco.size() * 4);
+  if (r == hipSuccess) r = dclo.ensure(clo.size() * 4);
   if (r == hipSuccess) r = pk.ensure((size_t)(n_pks ? n_pks : 1) * 96);
+  if (r == hipSuccess) r = acc.ensure((size_t)(nc ? nc : 1) * sizeof(g1j));
+  if (r == hipSuccess) r = cst.ensure((size_t)(nc ? nc : 1) * 4);
   if (r == hipSuccess) r = out.ensure((size_t)n_sets * 96);
   if (r == hipSuccess) r = stat.ensure((size_t)n_sets * 4);
-  if (r == hipSuccess)
-    r = hipMemcpyAsync(off.p, set_pk_offsets, (size_t)(n_sets + 1) * 4, hipMemcpyHostToDevice, e->stream);
+  if (r == hipSuccess) r = hipMemcpyAsync(dsco.p, sco.data(), sco.size() * 4, hipMemcpyHostToDevice, e->stream);
+  if (r == hipSuccess) r = hipMemcpyAsync(dclo.p, clo.data(), clo.size() * 4, hipMemcpyHostToDevice, e->stream);
   if (r == hipSuccess && n_pks) r = hipMemcpyAsync(pk.p, pubkeys, (size_t)n_pks * 96, hipMemcpyHostToDevice, e->stream);
   if (r == hipSuccess) {
-    hipLaunchKernelGGL(k_aggregate, dim3(nblk(n_sets)), dim3(LB_TPB), 0, e->stream, n_sets, off.as<uint32_t>(),
-                       pk.as<uint8_t>(), out.as<uint8_t>(), stat.as<int32_t>());
+    if (nc)
+      hipLaunchKernelGGL(k_pk_chunks, dim3(nblk(nc)), dim3(LB_TPB), 0, e->stream, nc, dclo.as<uint32_t>(), pk.as<uint8_t>(),
+                         acc.as<uint32_t>(), cst.as<int32_t>());
+    hipLaunchKernelGGL(k_pk_out96, dim3(nblk(n_sets)), dim3(LB_TPB), 0, e->stream, n_sets, nc, dsco.as<uint32_t>(),
+                       acc.as<uint32_t>(), cst.as<int32_t>(), out.as<uint8_t>(), stat.as<int32_t>());
     r = hipGetLastError();
   }
   if (r == hipSuccess) r = hipMemcpyAsync(out96, out.p, (size_t)n_sets * 96, hipMemcpyDeviceToHost, e->stream);
   if (r == hipSuccess) r = hipMemcpyAsync(out_status, stat.p, (size_t)n_sets * 4, hipMemcpyDeviceToHost, e->stream);
   if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
-  off.release();
-  pk.release();
-  out.release();
-  stat.release();
+  dbuf* tmp[] = {&dsco, &dclo, &pk, &acc, &cst, &out, &stat};
+  for (dbuf* d : tmp) d->release();
   if (r != hipSuccess) {
     fprintf(stderr, "lodestar_bls: aggregate failed: %s\n", hipGetErrorString(r));
     return LB_ERR_DEVICE;

@@ -2612,19 +2612,49 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_chunks(uint32_t n
 #ifndef LB_STRAUS_CHUNK
 #define LB_STRAUS_CHUNK 8
 #endif
+// The lanes take the chunks in order of decreasing member count (k_chunk_order: a counting sort
+// by size), so a wave's chunks have equal counts but at its edges and the member loop runs to the
+// wave's largest count: in root order the single-member roots' chunks (every aggregate-and-proof
+// root) shared waves with 8-member chunks and idled 7 of 8 additions (measured: the Straus form
+// 5 % below the per-set ladders before the ordering).
+#if LB_KG(14)
+__global__ void __launch_bounds__(LB_TPB) k_chunk_order(const uint32_t* __restrict__ n_u, const uint32_t* __restrict__ gch,
+                                                        const uint32_t* __restrict__ chunk_beg,
+                                                        const uint32_t* __restrict__ chunk_end,
+                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ order,
+                                                        uint32_t pass) {
+  // pass 0: cnt[m] = chunks of m members (m <= LB_STRAUS_CHUNK); pass 1: order (m descending),
+  // cnt[LB_STRAUS_CHUNK + 1 + m] the per-size cursors (zeroed with the counts)
+  const uint32_t c = lb_tid();
+  if (c >= gch[*n_u]) return;
+  const uint32_t m = chunk_end[c] - chunk_beg[c];
+  if (pass == 0) {
+    atomicAdd(&cnt[m], 1u);
+    return;
+  }
+  uint32_t base = 0;
+  for (uint32_t q = LB_STRAUS_CHUNK; q > m; q--) base += cnt[q];
+  order[base + atomicAdd(&cnt[LB_STRAUS_CHUNK + 1 + m], 1u)] = c;
+}
+#endif  // LB_KG
 #if LB_KG(14)
 __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_straus(uint32_t n, const uint32_t* __restrict__ n_u,
                                                         const uint32_t* __restrict__ gch,
                                                         const uint32_t* __restrict__ chunk_beg,
                                                         const uint32_t* __restrict__ chunk_end,
+                                                        const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ members,
                                                         const uint32_t* __restrict__ set_live,
                                                         const uint32_t* __restrict__ pk3,
                                                         const uint64_t* __restrict__ scalars,
                                                         uint32_t* __restrict__ gacc) {
-  const uint32_t c = lb_tid();
-  if (c >= gch[*n_u]) return;
-  const uint32_t b = chunk_beg[c], m = chunk_end[c] - b;
+  const uint32_t t = lb_tid(), nch = gch[*n_u];
+  if (blockIdx.x * LB_TPB >= nch) return;  // whole wave idle (uniform)
+  const bool act = t < nch;
+  const uint32_t c = act ? order[t] : 0u;
+  const uint32_t b = act ? chunk_beg[c] : 0u, m = act ? chunk_end[c] - b : 0u;
+  // the wave's largest count: its first lane's (decreasing order)
+  const uint32_t mw = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
   uint32_t idx[LB_STRAUS_CHUNK], lo[LB_STRAUS_CHUNK], hi[LB_STRAUS_CHUNK];
   LB_UNROLL for (int k = 0; k < LB_STRAUS_CHUNK; k++) {
     idx[k] = 0;
@@ -2644,6 +2674,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_straus(uint32_t n
   for (int bit = 31; bit >= 0; bit--) {
     if (!jac_is_inf(acc)) acc = jac_dbl_i(acc);
     LB_UNROLL for (int k = 0; k < LB_STRAUS_CHUNK; k++) {
+      if ((uint32_t)k >= mw) break;  // wave-uniform
       const uint32_t d = ((lo[k] >> bit) & 1u) | (((hi[k] >> bit) & 1u) << 1);
       if (d != 0u) {
         const g1x3 t = aos_ld<g1x3>(pk3, idx[k]);
@@ -2654,7 +2685,7 @@ __global__ void __launch_bounds__(LB_TPB, LB_MINW_GSUM) k_gsum_straus(uint32_t n
       }
     }
   }
-  soa_st(gacc, n, c, jac_as<fp>(acc));
+  if (act) soa_st(gacc, n, c, jac_as<fp>(acc));
 }
 #endif  // LB_KG
 
@@ -3000,26 +3031,28 @@ __global__ void __launch_bounds__(LBR_NT) k_partials_check_row(uint32_t n, const
 #endif  // LB_KG
 
 // ---------------------------------------------------------------- pubkey aggregation only
-#if LB_KG(0)
-__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_aggregate(uint32_t n, const uint32_t* __restrict__ pk_off,
-                                                      const uint8_t* __restrict__ pks, uint8_t* __restrict__ out96,
-                                                      int32_t* __restrict__ status) {
-  uint32_t i = lb_tid();
+// lb_aggregate_pubkeys (getAggregatedPubkey + toBytes(uncompressed), utils.ts:5-16,
+// multithread/index.ts:126,160) since round 6: k_pk_chunks' chunk sums with the segmented wave
+// tree, then per set the segment heads (first chunk, wave boundaries), affine, 96-byte encoding,
+// with the statuses of the round-5 one-lane-per-set form (first failing key in order; no key:
+// EMPTY_AGGREGATE_ARRAY) and its encoding of an infinite or failed aggregate (the infinity flag).
+#if LB_KG(14)
+__global__ void __launch_bounds__(LB_TPB, LB_MINW) k_pk_out96(uint32_t n, uint32_t nc, const uint32_t* __restrict__ set_chunk_off,
+                                                     const uint32_t* __restrict__ chunk_acc,
+                                                     const int32_t* __restrict__ chunk_status,
+                                                     uint8_t* __restrict__ out96, int32_t* __restrict__ status) {
+  const uint32_t i = lb_tid();
   if (i >= n) return;
-  uint32_t a = pk_off[i], e = pk_off[i + 1];
-  int st = (a == e) ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
+  const uint32_t c0 = set_chunk_off[i], c1 = set_chunk_off[i + 1];
+  int st = c0 == c1 ? LB_EMPTY_AGGREGATE_ARRAY : LB_OK;
   g1j acc = jac_infinity<fp>();
-  for (uint32_t k = a; k < e && st == LB_OK; k++) {
-    uint8_t b[96];
-    ld_bytes<96>(b, pks + (size_t)96 * k);
-    g1a p;
-    bool inf;
-    st = g1_deserialize96(b, p, inf);
-    if (st == LB_OK && !inf) acc = jac_add_aff(acc, p);
+  for (uint32_t c = c0; c < c1 && st == LB_OK; c++) {
+    st = chunk_status[c];
+    if (st == LB_OK && (c == c0 || (c & (LB_TPB - 1)) == 0)) acc = jac_add(acc, soa_ld<g1j>(chunk_acc, nc, c));
   }
   uint8_t ob[96];
   g1a r;
-  bool fin = jac_to_aff(r, acc);
+  const bool fin = jac_to_aff(r, acc);
   g1_serialize96(ob, r, !fin || st != LB_OK);
   for (int k = 0; k < 96; k++) out96[(size_t)96 * i + k] = ob[k];
   status[i] = st;

@@ -24,12 +24,13 @@ def main():
         took.append((free0 - torch.cuda.mem_get_info(0)[0]) / 2**20)
     print("MiB per engine creation:", " ".join("%.0f" % t for t in took), flush=True)
     wl = W.make(engines[0], "c1")
+    packs = [W.indexed_for(e, wl) for e in engines]  # each engine's own resident key table
     bad = []
 
-    def run(e):
-        if list(e.verify_jobs_packed(wl.packed)) != [int(x) for x in wl.expected]:
-            bad.append(1)
-    ths = [threading.Thread(target=run, args=(e,)) for e in engines]
+    def run(k):
+        if engines[k].verify_jobs_packed(packs[k]) != [int(x) for x in wl.expected]:
+            bad.append(k)
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(n)]
     for t in ths:
         t.start()
     for t in ths:

@@ -615,6 +615,10 @@ def test_search_term_forms_trace_the_same_rounds(monkeypatch, capfd):
     from lodestar_amd import workloads as W
     monkeypatch.setenv("LB_ROOT_SHUFFLE", "0")
     monkeypatch.setenv("LB_SEARCH_TRACE", "1")
+    # both runs with the under-load forms (LB_ALONE=0): an engine created right after another one
+    # closed saw the device as loaded, the first one as alone, and the look-ahead tests (alone
+    # only) changed the second round
+    monkeypatch.setenv("LB_ALONE", "0")
     traces = []
     for form in ("g8", "lane"):
         monkeypatch.setenv("LB_SMSM_FORM", form)

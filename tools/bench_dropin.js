@@ -7,7 +7,9 @@
 // timed on its own; the line reports the median round (>= 10 rounds, as the reference's
 // .benchrc.yaml minRuns), the GPU_MAX_HW_QUEUES the HIP runtime runs with, and the latency of a
 // 1-set verifyOnMainThread call (a gossip block's proposer check, validation/block.ts:143-146)
-// issued while a round of gossip batches is in flight.
+// issued while a round of gossip batches is in flight: its promise's settle time (the loop is
+// busy submitting the round meanwhile), the part of the call that runs on the loop (blocked), and
+// the synchronous entry's device latency on the same engine.
 //   node tools/bench_dropin.js <workload.bin> <engines> <rounds>
 // workload.bin (little-endian, written by bench.py): u32 magic 0x4C424430, n_keys, n_jobs, n_sets,
 // n_pks, slots; then keys (n_keys x 96 B), job_off (n_jobs+1 u32), pk_off (n_sets+1 u32),
@@ -103,6 +105,20 @@ async function main() {
   }
   lat.sort((a, b) => a - b);
   blocked.sort((a, b) => a - b);
+  // the same 1-set call through the synchronous entry (verifySignatureSet: the device latency on
+  // the latency engine, blocking the loop as the reference's verifyOnMainThread does): separates
+  // the device's latency under the pool's load from the event loop's queueing of the promise
+  const latSync = [];
+  for (let k = 0; k < 10; k++) {
+    const bg = round();
+    await new Promise((r) => setImmediate(r));
+    const c0 = process.hrtime.bigint();
+    const ok = pool.verifySignatureSet(one[0]);
+    latSync.push(Number(process.hrtime.bigint() - c0) / 1e6);
+    if (ok !== (expected[0] === 1)) throw Error("main-thread verdict (sync)");
+    await bg;
+  }
+  latSync.sort((a, b) => a - b);
   await pool.close();
   console.log(JSON.stringify({value_dropin: Math.round(nSets / med), value_dropin_mean: Math.round((nSets * rounds) / el),
                               seconds: Number(el.toFixed(3)), rounds, round_s_median: Number(med.toFixed(4)),
@@ -110,6 +126,7 @@ async function main() {
                               batches: stats.batches, mean_sets_per_batch: Math.round(stats.sets / Math.max(stats.batches, 1)),
                               main_thread_1set_ms_under_load: Number(lat[Math.floor(lat.length / 2)].toFixed(3)),
                               main_thread_1set_blocked_ms: Number(blocked[Math.floor(blocked.length / 2)].toFixed(3)),
+                              main_thread_1set_sync_ms_under_load: Number(latSync[Math.floor(latSync.length / 2)].toFixed(3)),
                               main_thread_1set_blocked_ms_max: Number(blocked[blocked.length - 1].toFixed(3))}));
 }
 

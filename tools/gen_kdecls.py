@@ -24,14 +24,14 @@ OUT = os.path.join(CSRC, "lb_kdecl.h")
 # kernel -> translation-unit group (balanced by measured compile time; the one-lane per-root and
 # decode kernels are the slow ones)
 GROUPS = {
-    0: ["k_decompress_sigs", "k_table_fill", "k_g1_decompress", "k_aggregate", "k_msg_insert", "k_dedup_one", "k_msg_uid_input",
+    0: ["k_decompress_sigs", "k_table_fill", "k_g1_decompress", "k_msg_insert", "k_dedup_one", "k_msg_uid_input",
         "k_msg_uid", "k_msg_count", "k_msg_scan", "k_chunk_fill", "k_msg_scatter", "k_job_status", "k_spec_live", "k_live_mismatch",
         "k_set_one", "k_g2_set_inf"],
     1: ["k_sig_subgroup", "k_sig_subgroup_g8", "k_sig_agg_chunks", "k_sig_agg_groups"],
     2: ["k_hash_map", "k_sk_to_pk", "k_sign", "k_ssz_zero_hashes", "k_merkleize"],
     3: ["k_hash_finish"],
     4: ["k_miller_lane", "k_pk_chunks", "k_pk_chunks_idx", "k_pk_blind", "k_gsum_chunks", "k_gsum_tree", "k_gsum_final"],
-    14: ["k_gsum_straus", "k_gsum_wave"],
+    14: ["k_chunk_order", "k_gsum_straus", "k_gsum_wave", "k_pk_out96"],
     5: ["k_miller_wave", "k_tree_up_U", "k_ml_S", "k_root_check", "k_root_partial", "k_partials_check", "k_search_ml",
         "k_search_fe", "k_search_match", "k_miller_g8", "k_kzg_check"],
     6: ["k_msm_count", "k_msm_scatter", "k_msm_chunks", "k_msm_buckets", "k_msm_reduce"],

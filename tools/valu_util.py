@@ -4,7 +4,7 @@
 
 Input: the counter_collection CSV of
     LB_PROF_MARK=1 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-        SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE -- python3 bench.py --steps K --inflight F ...
+        SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 GRBM_GUI_ACTIVE -- python3 bench.py ...
 bench.py brackets the headline's timed region with one k_partials_check dispatch each side
 (LB_PROF_MARK=1); only the dispatches between the two markers count, so "per batch" means one
 batch of the F-in-flight headline (K x F batches), without the workload generator (k_sign), the
@@ -16,6 +16,8 @@ Per kernel:
   valu_busy          SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the fraction of its waves' lifetime with a
                      VALU instruction issued (both in quad-cycles on gfx950, MI355X_MICROARCH.md)
   waves              SQ_WAVES per dispatch (mean)
+  int64_share        SQ_INSTS_VALU_INT64 / SQ_INSTS_VALU (64-bit integer VALU: the v_mad_u64_u32 of
+                     the Fp products, plus 64-bit adds / shifts)
 Chip:
   valu_issue_frac    the region's VALU wave-instructions x 2 cycles (wave64 VALU issue on a
                      SIMD-32, MI355X_MICROARCH.md "v_fma_f32 (wave64) 2 cyc") / (1 024 SIMDs x
@@ -75,6 +77,7 @@ def main():
            "valu_G_per_batch": round(tot["SQ_INSTS_VALU"] / a.batches / 1e9, 4),
            "salu_G_per_batch": round(tot.get("SQ_INSTS_SALU", 0.0) / a.batches / 1e9, 4),
            "valu_busy_all": round(tot["SQ_ACTIVE_INST_VALU"] / max(tot["SQ_WAVE_CYCLES"], 1.0), 4),
+           "int64_share_all": round(tot.get("SQ_INSTS_VALU_INT64", 0.0) / max(tot["SQ_INSTS_VALU"], 1.0), 4),
            "kernels": {}}
     for name, k in sorted(per.items(), key=lambda kv: -kv[1]["SQ_INSTS_VALU"]):
         out["kernels"][name] = {
@@ -84,6 +87,8 @@ def main():
             "valu_busy": round(k["SQ_ACTIVE_INST_VALU"] / max(k["SQ_WAVE_CYCLES"], 1.0), 4),
             "waves_per_dispatch": round(k["SQ_WAVES"] / k["dispatches"], 1),
         }
+        if "SQ_INSTS_VALU_INT64" in k:
+            out["kernels"][name]["int64_share"] = round(k["SQ_INSTS_VALU_INT64"] / max(k["SQ_INSTS_VALU"], 1.0), 4)
     if a.line:
         line = json.loads(open(a.line).read().strip().splitlines()[-1])
         t = line["ms_per_step"] * 1e-3  # seconds per batch of the headline, un-profiled
