@@ -695,9 +695,12 @@ def main():
         roof["chip_frac_note"] = ("sum of every stage's algorithmic Fp-mul x 300 MACs per batch / ms_per_step / "
                                   "peak: the headline's VALU utilisation, reproducible from this line alone")
         roof["stage_ms_source"] = ("HIP events on each stage's own stream, one batch in flight, %d profiled steps; "
-                                   "profiles/r5_rocprof_kernel_stats_inflight1.csv holds rocprof's per-kernel "
-                                   "averages for the same configuration; tools/trace_stage_avg.py -> "
-                                   "profiles/r5_inflight1_decode_check.json compares them" % a.steps)
+                                   "profiles/r6_rocprof_kernel_stats_inflight1.csv holds rocprof's per-kernel "
+                                   "averages for the same configuration (the round-6 final tree); "
+                                   "tools/trace_stage_avg.py -> profiles/r6_inflight1_decode_check.json compares them" % a.steps)
+        roof["valu_util_source"] = ("profiles/r6_valu_util.json: per-kernel VALU instructions per batch and VALU-busy "
+                                    "fraction from rocprofv3 counters at this configuration (tools/valu_util.py)")
+        roof["resource_table"] = "profiles/r6_resource_usage.txt (VGPR / AGPR / scratch / LDS per kernel, hipcc remarks)"
     segments = None
     if a.workload == "c3" and "segment" in a.legs.split(","):
         segments = segment_legs(a, eng, W, rank, world, barrier, coll_dev, backend)

@@ -149,8 +149,10 @@ struct lb_engine {
   uint32_t gmax_chunks = 0;  // chunks of the largest root (the k_gsum_tree levels), read back with n_u
   // under load (not alone) the per-root sums fold the blinding in, one Straus chain per chunk
   // (k_gsum_straus over pk3) instead of k_pk_blind's per-set ladder + the chunk sums; the per-set
-  // r PK (rpk) are then computed only if a search needs them (rpk_stale).  LB_GSUM_STRAUS=0: off
-  bool straus = true, straus_run = false, rpk_stale = false;
+  // r PK (rpk) are then computed only if a search needs them (rpk_stale).  LB_GSUM_STRAUS=1: on.
+  // Off by default: measured 4 % below the per-set ladders at 7 in flight even with the chunks in
+  // size order (10.53-10.59 M against 11.01-11.03 M sets/s, profiles/r6_straus_ab.txt)
+  bool straus = false, straus_run = false, rpk_stale = false;
   // a batch alone: the per-root sums' chunks combined by a segmented shuffle tree in one launch
   // (k_gsum_wave, chunks of LB_GROUP_CHUNK_WAVE) instead of the k_gsum_tree launches; LB_GSUM_WAVE=0
   bool gsum_wave = true;
@@ -201,6 +203,9 @@ struct lb_engine {
   // ... and with a workgroup per root on the row engine while the device is alone.  LB_HASH_ROW_MAX.
   uint32_t hash_row_max = 256;
   uint32_t hash_row_careful = 0;  // LB_HASH_ROW_CAREFUL=1: the exceptional-case path always (tests)
+  // round 6: the row forms' G2 chains (cofactor clearing, the subgroup ladder, r_i sig_i) in
+  // projective coordinates with the complete formulas; LB_ROW_PROJ=0: the Jacobian programs
+  bool row_proj = true;
   // ... and the signature decode's square roots on rows up to this many sets.  LB_DEC_ROW_MAX.
   uint32_t dec_row_max = 4096;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
@@ -454,6 +459,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   if (const char* hr = getenv("LB_HASH_ROW_MAX")) e->hash_row_max = (uint32_t)strtoul(hr, nullptr, 10);
   if (const char* dr = getenv("LB_DEC_ROW_MAX")) e->dec_row_max = (uint32_t)strtoul(dr, nullptr, 10);
   if (const char* hc = getenv("LB_HASH_ROW_CAREFUL")) e->hash_row_careful = (uint32_t)strtoul(hc, nullptr, 10);
+  if (const char* rp = getenv("LB_ROW_PROJ")) e->row_proj = std::atoi(rp) != 0;
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
   if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
@@ -1120,7 +1126,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
       if (n <= e->row_max && e->alone && e->row_fe)
         hipLaunchKernelGGL(k_sig_subgroup_row, dim3(n), dim3(LBR_NT), 0, s2, n, e->sig_aff.as<uint32_t>(),
-                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(), e->row_proj ? 1u : 0u);
       else if (n <= e->subgroup_g8_max)
         hipLaunchKernelGGL(k_sig_subgroup_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
@@ -1198,7 +1204,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       const bool alone = e->miller_form == 0 && device_alone(e);
       if (nuh <= e->hash_row_max && e->alone && e->row_fe)
         hipLaunchKernelGGL(k_hash_finish_row, dim3(nuh), dim3(LBR_NT), 0, s1, n, nu, e->q.as<uint32_t>(),
-                           e->h_aff.as<uint32_t>(), e->hash_row_careful);
+                           e->h_aff.as<uint32_t>(), e->hash_row_careful ? 1u : (e->row_proj ? 0u : 2u));
       else if (nuh <= e->hash_g8_max || (LB_HASH_ALONE_G8 && alone))
         hipLaunchKernelGGL(k_hash_finish_g8, dim3((nuh + 7) / 8), dim3(64), 0, s1, n, nu, e->q.as<uint32_t>(),
                            e->h_aff.as<uint32_t>());
@@ -1222,7 +1228,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       if (n <= e->row_max && e->alone && e->row_fe)
         hipLaunchKernelGGL(k_sig_blind_row, dim3(n), dim3(LBR_NT), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),
-                           e->s_terms.as<uint32_t>());
+                           e->s_terms.as<uint32_t>(), e->row_proj ? 1u : 0u);
       else if (n <= e->small_s_g8_max)
         hipLaunchKernelGGL(k_sig_blind_g8, dim3((n + 7) / 8), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->scalars.as<uint64_t>(), e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(),

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(64) k_sig_subgroup_g8(uint32_t n, const uint32
 #if LB_KG(12)
 __global__ void __launch_bounds__(LBR_NT) k_sig_subgroup_row(uint32_t n, const uint32_t* __restrict__ sig_aff,
                                                            const uint32_t* __restrict__ sig_inf,
-                                                           int32_t* __restrict__ sig_status) {
+                                                           int32_t* __restrict__ sig_status, uint32_t proj) {
   LBR_SHARED_N(S, LBR_PROGS_END - LBR_G2DBL);
   const uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -353,6 +353,19 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_subgroup_row(uint32_t n, const u
     }
     r_sync();
     r_import_staged(S, P, 6);
+  }
+  if (proj) {
+    // round 6: the [|x|] ladder in projective coordinates with the complete formulas (no
+    // exceptional case, no rerun), then psi(P) = -acc <=> X1 Z2 = X2 Z1 and Y1 Z2 = -Y2 Z1 (PEQN;
+    // an infinite acc leaves Y2 Z1 != 0)
+    r_run(S, &LBR_OPS_XLADDER_P, LBR_OPS_XLADDER_P.n);
+    r_g2_psi(S, PSI, P);
+    r_gather(S, LBR_IN, 12, [&](int e) { return e < 6 ? PSI + e : X + e - 6; });
+    r_exec(S, LBR_PEQN);
+    const lds_i32* pq = r_progs(S) + LBR_PEQN;
+    const uint32_t mz = r_zero_mask(S, 4, [&](int e) { return pq[2 + e]; });
+    if (r_tid() == 0 && mz != 0xf) sig_status[i] = LB_POINT_NOT_IN_GROUP;
+    return;
   }
   r_run(S, &LBR_OPS_XLADDER, LBR_OPS_XLADDER.n);
   if (r_zero_mask(S, 2, [&](int e) { return X + 4 + e; }) == 3) r_g2_mul_xabs<false>(S, X, P);
@@ -814,13 +827,23 @@ __global__ void __launch_bounds__(LBR_NT) k_hash_finish_row(uint32_t n, const ui
     r_sync();
     r_import_staged(S, Q0, 12);
   }
-  r_copy(S, LBR_A(5), Q0, 12);  // Q0, Q1 kept for a recomputation
-  r_run(S, &LBR_OPS_HASH, LBR_OPS_HASH.n);  // Q0 + Q1, cofactor clearing into H (fast path)
-  // Z = 0 (or `careful`, LB_HASH_ROW_CAREFUL for the tests): again with the tests
-  if (r_zero_mask(S, 2, [&](int e) { return H + 4 + e; }) == 3 || careful) {
-    r_copy(S, Q0, LBR_A(5), 12);
-    r_g2_add(S, Q0, Q0, Q1);
-    r_g2_clear_cofactor<false>(S, H, Q0);
+  // careful bit 0 (LB_HASH_ROW_CAREFUL, tests): the Jacobian chain with the exceptional-case
+  // tests; bit 1 (LB_ROW_PROJ=0): the Jacobian fast chain (rerun with the tests on Z = 0).
+  // Default (round 6): projective coordinates, complete additions, no rerun.
+  const bool proj = careful == 0;
+  if (proj) {
+    r_g2_prog(S, LBR_JTOP, Q0, Q0);
+    r_g2_prog(S, LBR_JTOP, Q1, Q1);
+    r_run(S, &LBR_OPS_HASH_P, LBR_OPS_HASH_P.n);  // Q0 + Q1, cofactor clearing into H
+  } else {
+    r_copy(S, LBR_A(5), Q0, 12);  // Q0, Q1 kept for a recomputation
+    r_run(S, &LBR_OPS_HASH, LBR_OPS_HASH.n);  // Q0 + Q1, cofactor clearing into H (fast path)
+    // Z = 0 (or `careful` bit 0, LB_HASH_ROW_CAREFUL for the tests): again with the tests
+    if (r_zero_mask(S, 2, [&](int e) { return H + 4 + e; }) == 3 || (careful & 1)) {
+      r_copy(S, Q0, LBR_A(5), 12);
+      r_g2_add(S, Q0, Q0, Q1);
+      r_g2_clear_cofactor<false>(S, H, Q0);
+    }
   }
   r_export(S, H, 6);
   if (r_tid() == 0) {
@@ -836,9 +859,14 @@ __global__ void __launch_bounds__(LBR_NT) k_hash_finish_row(uint32_t n, const ui
     } else {
       const fp ni = fp_inv_i(nz);
       const fp2 zi{fp_mul(h.z.c0, ni), fp_neg(fp_mul(h.z.c1, ni))};
-      const fp2 zi2 = fp2_sqr(zi);
-      a.x = fp2_mul(h.x, zi2);
-      a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
+      if (proj) {  // x = X / Z, y = Y / Z
+        a.x = fp2_mul(h.x, zi);
+        a.y = fp2_mul(h.y, zi);
+      } else {  // x = X / Z^2, y = Y / Z^3
+        const fp2 zi2 = fp2_sqr(zi);
+        a.x = fp2_mul(h.x, zi2);
+        a.y = fp2_mul(fp2_mul(h.y, zi2), zi);
+      }
     }
     soa_st(h_aff, n, u, a);
   }
@@ -1884,7 +1912,7 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_blind_row(uint32_t n, const uint
                                                         const uint64_t* __restrict__ scalars,
                                                         const uint32_t* __restrict__ set_live,
                                                         const uint32_t* __restrict__ sig_inf,
-                                                        uint32_t* __restrict__ terms) {
+                                                        uint32_t* __restrict__ terms, uint32_t proj) {
   LBR_SHARED_N(S, LBR_PROGS_END - LBR_G2DBL);
   const uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -1909,7 +1937,11 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_blind_row(uint32_t n, const uint
   }
   r_g2_psi2(S, T2, T1);
   r_g2_neg(S, T2);  // [lambda] sig = -psi^2(sig)
-  r_g2_add(S, T3, T1, T2);
+  // proj (round 6): the table and the ladder in projective coordinates with the complete
+  // formulas (T1 = (x : y : 1) as it is; psi^2 and the negation act the same), the result back
+  // to Jacobian (PTOJ) for the S sum
+  if (proj) r_g2_prog(S, LBR_PADD, T3, T1, T2);
+  else r_g2_add(S, T3, T1, T2);
   const uint64_t w = scalars[i];
   const uint32_t k0 = (uint32_t)w, k1 = (uint32_t)(w >> 32);
   auto digit = [&](int b) { return ((k0 >> b) & 1u) | (((k1 >> b) & 1u) << 1); };
@@ -1922,10 +1954,16 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_blind_row(uint32_t n, const uint
   auto tab = [&](uint32_t d) { return d == 1 ? T1 : (d == 2 ? T2 : T3); };
   r_copy(S, ACC, tab(digit(b)), 6);
   for (b--; b >= 0; b--) {
-    r_g2_dbl(S, ACC, ACC);
     const uint32_t d = digit(b);
-    if (d) r_g2_add(S, ACC, ACC, tab(d));
+    if (proj) {
+      r_g2_prog(S, LBR_PDBL1, ACC, ACC);
+      if (d) r_g2_prog(S, LBR_PADD, ACC, ACC, tab(d));
+    } else {
+      r_g2_dbl(S, ACC, ACC);
+      if (d) r_g2_add(S, ACC, ACC, tab(d));
+    }
   }
+  if (proj) r_g2_prog(S, LBR_PTOJ, ACC, ACC);
   r_export(S, ACC, 6);
   if (threadIdx.x < 6) {
     const fp v = r_fp_of_staged(S, threadIdx.x);

@@ -827,6 +827,12 @@ enum {
   RK_CONJ,   // dst = conj(a) (Fp12)
   RK_COPY,   // dst[0, b) = a[0, b)
   RK_G2NEG,  // a = -a (G2)
+  // round 6: homogeneous projective G2 with the complete formulas (gen_row_programs.py g2_pdbl /
+  // g2_padd: 2 product levels per doubling and per addition, no exceptional cases)
+  RK_PDBL,   // dst = 2a
+  RK_PDBL2,  // dst = 4a
+  RK_PDBL4,  // dst = 16a
+  RK_PADD,   // dst = a + b (complete)
 };
 #define LBR_MAX_OPS 400
 struct r_opl {
@@ -838,20 +844,24 @@ struct r_opl {
     n++;
   }
   // dst = a^|x| (a cyclotomic, dst != a)
+  constexpr void csqrs(int dst, int run) {  // run chained squarings, two per program
+    // (4 or 8 chained squarings in one program measured 8 / 21 phases in the generator: the
+    // operand sums outgrow the flattening bound; two per program, 3 phases, stays the best)
+    for (; run >= 2; run -= 2) op(RK_CSQR2, dst, dst);
+    if (run) op(RK_CSQR, dst, dst);
+  }
   constexpr void pow_xabs(int dst, int a) {
     op(RK_COPY, dst, a, 12);
-    int run = 0;  // squarings pending (issued two at a time)
+    int run = 0;  // squarings pending
     for (int i = 62; i >= 0; i--) {
       run++;
       if ((LB_X_ABS >> i) & 1ull) {
-        for (; run >= 2; run -= 2) op(RK_CSQR2, dst, dst);
-        if (run) op(RK_CSQR, dst, dst);
+        csqrs(dst, run);
         run = 0;
         op(RK_MUL, dst, dst, a);
       }
     }
-    for (; run >= 2; run -= 2) op(RK_CSQR2, dst, dst);
-    if (run) op(RK_CSQR, dst, dst);
+    csqrs(dst, run);
   }
   // dst = [|x|] a (G2, dst != a)
   constexpr void g2_dbls(int dst, int run) {
@@ -871,6 +881,25 @@ struct r_opl {
       }
     }
     g2_dbls(dst, run);
+  }
+  // the same in projective coordinates (complete additions)
+  constexpr void p_dbls(int dst, int run) {
+    for (; run >= 4; run -= 4) op(RK_PDBL4, dst, dst);
+    for (; run >= 2; run -= 2) op(RK_PDBL2, dst, dst);
+    if (run) op(RK_PDBL, dst, dst);
+  }
+  constexpr void p_mul_xabs(int dst, int a) {
+    op(RK_COPY, dst, a, 6);
+    int run = 0;
+    for (int i = 62; i >= 0; i--) {
+      run++;
+      if ((LB_X_ABS >> i) & 1ull) {
+        p_dbls(dst, run);
+        run = 0;
+        op(RK_PADD, dst, dst, a);
+      }
+    }
+    p_dbls(dst, run);
   }
 };
 // r_final_exp after the inversion (Y0 = f^-1): the chain of lb_pairing.h final_exponentiation
@@ -936,6 +965,39 @@ constexpr r_opl r_ops_hash_finish(int dst, int q) {
   o.op(RK_G2ADD, dst, T3, W);
   return o;
 }
+// the same chain in projective coordinates with the complete additions (k_hash_finish_row's
+// default since round 6; q .. q + 11 projective): no exceptional case, so no rerun
+constexpr r_opl r_ops_hash_finish_p(int dst, int q) {
+  r_opl o;
+  const int T1 = LBR_A(0), T3 = LBR_A(0) + 6, T2 = LBR_A(1), X = LBR_A(1) + 6, W = LBR_A(2);
+  const int p = q;
+  o.op(RK_PADD, p, q, q + 6);
+  o.p_mul_xabs(T1, p);
+  o.op(RK_G2NEG, T1, T1);
+  o.op(RK_PDBL, T3, p);
+  o.op(RK_PSI2, T3, T3);
+  o.op(RK_PSI, T2, p);
+  o.op(RK_COPY, W, T2, 6);
+  o.op(RK_G2NEG, W, W);
+  o.op(RK_PADD, T3, T3, W);
+  o.op(RK_PADD, T2, T2, T1);
+  o.p_mul_xabs(X, T2);
+  o.op(RK_G2NEG, X, X);
+  o.op(RK_PADD, T3, T3, X);
+  o.op(RK_G2NEG, T1, T1);
+  o.op(RK_PADD, T3, T3, T1);
+  o.op(RK_COPY, W, p, 6);
+  o.op(RK_G2NEG, W, W);
+  o.op(RK_PADD, dst, T3, W);
+  return o;
+}
+constexpr r_opl r_ops_xladder_p(int dst, int p) {
+  r_opl o;
+  o.p_mul_xabs(dst, p);
+  return o;
+}
+static __device__ const r_opl LBR_OPS_HASH_P = r_ops_hash_finish_p(LBR_A(4), LBR_A(3));
+static __device__ const r_opl LBR_OPS_XLADDER_P = r_ops_xladder_p(LBR_A(4), LBR_A(3));
 static __device__ const r_opl LBR_OPS_FE_A0 = r_ops_fe_tail(LBR_A(0), LBR_A(0));
 static __device__ const r_opl LBR_OPS_ML_A0 = r_ops_miller(LBR_A(0));
 static __device__ const r_opl LBR_OPS_ML_A7 = r_ops_miller(LBR_A(7));
@@ -985,10 +1047,14 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
       case RK_G2ADD: prog = LBR_G2ADD; na = 6; nb = 6; nout = 6; break;
       case RK_PSI: prog = LBR_PSI; na = 6; nb = 0; nout = 6; break;
       case RK_PSI2: prog = LBR_PSI2; na = 6; nb = 0; nout = 6; break;
+      case RK_PDBL: prog = LBR_PDBL1; na = 6; nb = 0; nout = 6; break;
+      case RK_PDBL2: prog = LBR_PDBL2; na = 6; nb = 0; nout = 6; break;
+      case RK_PDBL4: prog = LBR_PDBL4; na = 6; nb = 0; nout = 6; break;
+      case RK_PADD: prog = LBR_PADD; na = 6; nb = 6; nout = 6; break;
       case RK_MLDBL: prog = LBR_DBL_STEP; na = 12; nb = 0; nout = 18; break;
       default: prog = LBR_ADD_STEP; na = 12; nb = 0; nout = 18; break;  // RK_MLADD
     }
-    const bool ml = kind >= RK_MLDBL;
+    const bool ml = kind == RK_MLDBL || kind == RK_MLADD;
     const int src_a = ml ? dst : a;
     // inputs into IN (sources never in IN: one barrier)
     const int nin = ml ? (kind == RK_MLDBL ? 20 : 24) : na + nb;
@@ -1154,6 +1220,12 @@ __device__ void r_g2_dbl(int32_t* S, int dst, int a) {
   r_copy(S, LBR_IN, a, 6);
   r_exec(S, LBR_G2DBL);
   r_out(S, LBR_G2DBL, 0, 6, dst);
+}
+// a 6-slot G2 program: dst = prog(a) or prog(a, b) (b: a second 6-slot input, -1 for none)
+__device__ void r_g2_prog(int32_t* S, int prog, int dst, int a, int b = -1) {
+  r_gather(S, LBR_IN, b < 0 ? 6 : 12, [&](int e) { return e < 6 ? a + e : b + e - 6; });
+  r_exec(S, prog);
+  r_out(S, prog, 0, 6, dst);
 }
 __device__ void r_g2_psi(int32_t* S, int dst, int a) {
   r_copy(S, LBR_IN, a, 6);

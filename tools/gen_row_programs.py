@@ -255,6 +255,73 @@ def g2_add(t, P, Q):
     return (X3, Y3, Z3), H, r
 
 
+# ---- homogeneous projective G2 (x = X / Z, y = Y / Z), the complete a = 0 formulas of Renes,
+# Costello and Batina (2016; Algorithms 7 and 9).  E'(Fp2) has odd order (no 2-torsion), so
+# they have no exceptional case: the identity is (0 : Y : 0), P = Q and P = -Q need no tests.
+# On the row engine a phase costs ~1 us against a product's 0.45 us, so what counts is product
+# LEVELS: the doubling needs 2 (Jacobian dbl-2009-l: 3), the addition 2 (add-2007-bl: 6).
+def f2b3(t, a):
+    """b3 a with b3 = 3 b = 12 (1 + u) on E': y^2 = x^3 + 4 (1 + u): linear"""
+    x = t.f2xi(a)
+    return (x[0].scale(12), x[1].scale(12))
+
+
+def g2_pdbl(t, P):
+    """2P, RCB Algorithm 9: products Y^2, YZ, Z^2, XY, then 4 products of level 2"""
+    X, Y, Z = P
+    t0 = t.f2sqr(Y)
+    t1 = t.f2mul(Y, Z)
+    t2 = f2b3(t, t.f2sqr(Z))
+    z8 = (t0[0].scale(8), t0[1].scale(8))
+    x3a = t.f2mul(t2, z8)
+    y3s = t.f2add(t0, t2)
+    Z3 = t.f2mul(t1, z8)
+    t0m = t.f2sub(t0, t.f2mul3(t2))
+    Y3 = t.f2add(x3a, t.f2mul(t0m, y3s))
+    X3 = t.f2dbl(t.f2mul(t0m, t.f2mul(X, Y)))
+    return X3, Y3, Z3
+
+
+def g2_padd(t, P, Q):
+    """P + Q, RCB Algorithm 7 (complete): 6 products, then 6 products"""
+    X1, Y1, Z1 = P
+    X2, Y2, Z2 = Q
+    t0 = t.f2mul(X1, X2)
+    t1 = t.f2mul(Y1, Y2)
+    t2 = t.f2mul(Z1, Z2)
+    t3 = t.f2sub(t.f2mul(t.f2add(X1, Y1), t.f2add(X2, Y2)), t.f2add(t0, t1))
+    t4 = t.f2sub(t.f2mul(t.f2add(Y1, Z1), t.f2add(Y2, Z2)), t.f2add(t1, t2))
+    sxz = t.f2sub(t.f2mul(t.f2add(X1, Z1), t.f2add(X2, Z2)), t.f2add(t0, t2))
+    t0x3 = t.f2mul3(t0)
+    t2b = f2b3(t, t2)
+    z3a = t.f2add(t1, t2b)
+    t1m = t.f2sub(t1, t2b)
+    y3b = f2b3(t, sxz)
+    X3 = t.f2sub(t.f2mul(t3, t1m), t.f2mul(t4, y3b))
+    Y3 = t.f2add(t.f2mul(t1m, z3a), t.f2mul(y3b, t0x3))
+    Z3 = t.f2add(t.f2mul(z3a, t4), t.f2mul(t0x3, t3))
+    return X3, Y3, Z3
+
+
+def g2_jtop(t, P):
+    """Jacobian (X, Y, Z) -> projective (X Z, Y, Z^3)"""
+    X, Y, Z = P
+    return t.f2mul(X, Z), Y, t.f2mul(t.f2sqr(Z), Z)
+
+
+def g2_ptoj(t, P):
+    """projective (X, Y, Z) -> Jacobian (X Z, Y Z^2, Z)"""
+    X, Y, Z = P
+    return t.f2mul(X, Z), t.f2mul(Y, t.f2sqr(Z)), Z
+
+
+def g2_peqn(t, A, B):
+    """(X1 Z2 - X2 Z1, Y1 Z2 + Y2 Z1): both zero iff A = -B for finite A (B = O gives Y2 Z1)"""
+    X1, Y1, Z1 = A
+    X2, Y2, Z2 = B
+    return t.f2sub(t.f2mul(X1, Z2), t.f2mul(X2, Z1)), t.f2add(t.f2mul(Y1, Z2), t.f2mul(Y2, Z1))
+
+
 def g2_psi(t, pg, P):
     X, Y, Z = P
     cx = (pg.const(C_PSI_CX), pg.const(C_PSI_CX + 1))
@@ -314,6 +381,32 @@ def build_programs():
                 P = g2_dbl(t, P)
             pg.output(g2_flat(P))
             progs["G2DBL%d" % k] = pg
+        # round 6: projective (complete) point programs
+        for k in (1, 2, 4):
+            pg = RowProg("PDBL%d" % k)
+            t = G.T(pg)
+            P = g2_in(pg, 0)
+            for _ in range(k):
+                P = g2_pdbl(t, P)
+            pg.output(g2_flat(P))
+            progs["PDBL%d" % k] = pg
+        pg = RowProg("PADD")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_padd(t, g2_in(pg, 0), g2_in(pg, 6))))
+        progs["PADD"] = pg
+        pg = RowProg("JTOP")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_jtop(t, g2_in(pg, 0))))
+        progs["JTOP"] = pg
+        pg = RowProg("PTOJ")
+        t = G.T(pg)
+        pg.output(g2_flat(g2_ptoj(t, g2_in(pg, 0))))
+        progs["PTOJ"] = pg
+        pg = RowProg("PEQN")
+        t = G.T(pg)
+        e1, e2 = g2_peqn(t, g2_in(pg, 0), g2_in(pg, 6))
+        pg.output(list(e1) + list(e2))
+        progs["PEQN"] = pg
     finally:
         G.Prog = saved
     return progs
@@ -553,6 +646,59 @@ def _checks(codes):
         assert g2_row_out(got) == o.g2_mul(Pa, 16), "G2DBL4"
         got = [from_row(v) for v in run_row(codes["G2DBL2"].words, S)]
         assert g2_row_out(got) == o.g2_mul(Pa, 4), "G2DBL2"
+    # projective programs: random representatives (x z, y z, z), results read as (X / Z, Y / Z)
+    def p_in(Pa):
+        z = (rnd.randrange(1, P), rnd.randrange(P))
+        return [c for v in (o.f2_mul(Pa[0], z), o.f2_mul(Pa[1], z), z) for c in v]
+
+    def p_out(v):
+        X, Y, Z = (v[0], v[1]), (v[2], v[3]), (v[4], v[5])
+        if Z == (0, 0):
+            return None
+        zi = o.f2_inv(Z)
+        return (o.f2_mul(X, zi), o.f2_mul(Y, zi))
+    for k in range(2):
+        Pa = o.hash_to_g2(bytes([k, 3]) * 16)
+        Qa = o.hash_to_g2(bytes([k, 4]) * 16)
+        for a, b, want in ((Pa, Qa, o.g2_add(Pa, Qa)), (Pa, Pa, o.g2_add(Pa, Pa)), (Pa, o.g2_neg(Pa), None)):
+            S = dict(base)
+            S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(p_in(a) + p_in(b))})
+            got = [from_row(v) for v in run_row(codes["PADD"].words, S)]
+            assert p_out(got) == want, "PADD"
+        S = dict(base)
+        S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(p_in(Pa) + p_in(Qa))})
+        got = [from_row(v) for v in run_row(codes["PDBL1"].words, S)]
+        assert p_out(got) == o.g2_add(Pa, Pa), "PDBL1"
+        got = [from_row(v) for v in run_row(codes["PDBL2"].words, S)]
+        assert p_out(got) == o.g2_mul(Pa, 4), "PDBL2"
+        got = [from_row(v) for v in run_row(codes["PDBL4"].words, S)]
+        assert p_out(got) == o.g2_mul(Pa, 16), "PDBL4"
+        got = [from_row(v) for v in run_row(codes["PTOJ"].words, S)]
+        assert g2_row_out(got) == Pa, "PTOJ"
+        got = [from_row(v) for v in run_row(codes["PSI"].words, S)]
+        assert p_out(got) == o.g2_psi(Pa), "PSI (projective)"
+        got = [from_row(v) for v in run_row(codes["PSI2"].words, S)]
+        assert p_out(got) == o.g2_psi(o.g2_psi(Pa)), "PSI2 (projective)"
+        S = dict(base)
+        S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(g2_row_in(Pa))})
+        got = [from_row(v) for v in run_row(codes["JTOP"].words, S)]
+        assert p_out(got) == Pa, "JTOP"
+        for b, zero in ((o.g2_neg(Pa), True), (Pa, False), (Qa, False)):
+            S = dict(base)
+            S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(p_in(Pa) + p_in(b))})
+            got = [from_row(v) for v in run_row(codes["PEQN"].words, S)]
+            assert (got == [0, 0, 0, 0]) == zero, "PEQN"
+        # the identity (0 : 1 : 0) on either side of the complete addition and the doubling
+        S = dict(base)
+        S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate(p_in(Pa) + [0, 0, 1, 0, 0, 0])})
+        got = [from_row(v) for v in run_row(codes["PADD"].words, S)]
+        assert p_out(got) == Pa, "PADD P + O"
+        S = dict(base)
+        S.update({G.IN_BASE + j: to_row(v) for j, v in enumerate([0, 0, 1, 0, 0, 0] + p_in(Pa))})
+        got = [from_row(v) for v in run_row(codes["PADD"].words, S)]
+        assert p_out(got) == Pa, "PADD O + P"
+        got = [from_row(v) for v in run_row(codes["PDBL1"].words, S)]
+        assert p_out(got) is None, "PDBL1 O"
     # a few Miller steps against the lone-lane programs' interpreter (values, not limbs)
     Pp = o.sk_to_pk(0x1234567)
     Qq = o.hash_to_g2(b"\x07" * 32)
@@ -569,7 +715,8 @@ def _checks(codes):
         assert got == want, name
 
 
-ORDER = ["MUL12", "SQR12", "CSQR12", "CSQR12X2", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2", "G2DBL2", "G2DBL4"]
+ORDER = ["MUL12", "SQR12", "CSQR12", "CSQR12X2", "FROB", "FROB2", "DBL_STEP", "ADD_STEP", "G2DBL", "G2ADD", "PSI", "PSI2", "G2DBL2", "G2DBL4",
+         "PDBL1", "PDBL2", "PDBL4", "PADD", "JTOP", "PTOJ", "PEQN"]
 
 
 def const_limbs(v):

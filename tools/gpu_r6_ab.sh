@@ -17,5 +17,5 @@ for r in $RUNS; do
   tag=$i_$(echo "$r" | tr ':=/@+' '_____')
   if [ -n "$LEGS" ]; then legs="--legs $LEGS"; else legs="--no-extra"; fi
   env $envs timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline ${BENCH_FLAGS:---no-distinct} $legs > $OUT/$i.$tag.log 2>&1 || { tail -5 $OUT/$i.$tag.log; exit 1; }
-  echo "== $r"; tail -1 $OUT/$i.$tag.log | python3 tools/bench_summary.py | head -${NLINES:-3}
+  echo "== $r"; tail -1 $OUT/$i.$tag.log | python3 tools/bench_summary.py > $OUT/$i.summary.txt; head -${NLINES:-3} $OUT/$i.summary.txt
 done
