@@ -556,15 +556,22 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
         // lane), the 8-lane subgroup check and r_i sig_i of small batches (616 / 868 B); s3 the
         // 96-byte-key chunk sums (584 B).  The rest of s2 / s3's kernels need less per lane and
         // fewer lanes (resource table: DESIGN.md section 5.2).
-        hipLaunchKernelGGL(k_decompress_sigs, dim3(4096), dim3(LB_TPB), 0, e->stream2, 0u, nullptr, nullptr, nullptr,
-                           nullptr, nullptr, nullptr);
-        // (one wave per 8 sets, at least one wave, at most 16 384: more than the device holds)
-        auto g8_waves = [](uint32_t sets) { return dim3(std::min<uint32_t>(16384u, std::max<uint32_t>(1u, sets / 8 + 1))); };
-        hipLaunchKernelGGL(k_sig_subgroup_g8, g8_waves(e->subgroup_g8_max), dim3(64), 0, e->stream2, 0u, nullptr, nullptr,
-                           nullptr);
-        hipLaunchKernelGGL(k_sig_blind_g8, g8_waves(e->small_s_g8_max), dim3(64), 0, e->stream2, 0u, nullptr, nullptr,
-                           nullptr, nullptr, nullptr);
-        hipLaunchKernelGGL(k_pk_chunks, dim3(4096), dim3(LB_TPB), 0, e->stream3, 0u, nullptr, nullptr, nullptr, nullptr);
+        // LB_RESERVE_S23 (A/B): 0 none, 1 the decode + s3 only, 2 (default) all of the above
+        const char* rv = getenv("LB_RESERVE_S23");
+        const int res23 = rv ? atoi(rv) : 2;
+        if (res23 >= 1) {
+          hipLaunchKernelGGL(k_decompress_sigs, dim3(4096), dim3(LB_TPB), 0, e->stream2, 0u, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, nullptr);
+          hipLaunchKernelGGL(k_pk_chunks, dim3(4096), dim3(LB_TPB), 0, e->stream3, 0u, nullptr, nullptr, nullptr, nullptr);
+        }
+        if (res23 >= 2) {
+          // (one wave per 8 sets, at least one wave, at most 16 384: more than the device holds)
+          auto g8_waves = [](uint32_t sets) { return dim3(std::min<uint32_t>(16384u, std::max<uint32_t>(1u, sets / 8 + 1))); };
+          hipLaunchKernelGGL(k_sig_subgroup_g8, g8_waves(e->subgroup_g8_max), dim3(64), 0, e->stream2, 0u, nullptr,
+                             nullptr, nullptr);
+          hipLaunchKernelGGL(k_sig_blind_g8, g8_waves(e->small_s_g8_max), dim3(64), 0, e->stream2, 0u, nullptr, nullptr,
+                             nullptr, nullptr, nullptr);
+        }
         ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(e->stream) == hipSuccess &&
              hipStreamSynchronize(e->stream2) == hipSuccess && hipStreamSynchronize(e->stream3) == hipSuccess;
       }

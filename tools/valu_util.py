@@ -60,7 +60,9 @@ def main():
     marks = [d for d, e in rows.items() if e["name"].startswith(MARK)]
     if len(marks) < 2:
         sys.exit("need the two LB_PROF_MARK dispatches (k_partials_check) in the trace")
-    lo, hi = marks[-2], marks[-1]
+    # the FIRST pair: the headline's region (bench.py's later legs -- the range-sync segments --
+    # call lb_fp12_product_is_one too)
+    lo, hi = marks[0], marks[1]
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     tot = collections.defaultdict(float)
     for d, e in rows.items():
