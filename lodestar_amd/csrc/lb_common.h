@@ -12,6 +12,12 @@
 #endif
 #define LB_KG(g) (LB_KGROUP < 0 || LB_KGROUP == (g))
 
+// k_hash_map_row: map_to_curve_g2_fold on row pairs (1) or map_to_curve_g2_i on single rows (0, A/B);
+// k_decompress_sigs_row: its square roots' exponentiations on row pairs (1) or single rows (0)
+#ifndef LB_H2C_FOLD
+#define LB_H2C_FOLD 1
+#endif
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define LB_HD __host__ __device__ __forceinline__

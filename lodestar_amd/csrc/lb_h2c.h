@@ -197,6 +197,82 @@ LB_NI g2j map_to_curve_g2(fp2 u) {
   return r;
 }
 
+// The same map with the SSWU denominator's inversion and gx1's Legendre symbol folded into the
+// square root's first exponentiation, so the chain is two exponentiations by (p - 3) / 4 and a
+// few dozen products (map_to_curve_g2 above: an Fp2 inversion, a Jacobi symbol, then the two
+// exponentiations).  `pow(a, LB_EXP_ISQRT, 378)` returns a^((p-3)/4); the output is the same
+// Jacobian point as map_to_curve_g2 (same affine x, y; Z = xden yden).
+//   x1 = N / D (projective SSWU), gx1 = U / V with U = N^3 + A N D^2 + B D^3, V = D^3;
+//   t = nu nv^3 (nu = norm U, nv = norm V), w = t^((p-3)/4), chi = w^2 t = t^((p-1)/2):
+//     chi = legendre(norm gx1) (gx1 is a square in Fp2 iff its norm is one in Fp, or gx1 = 0),
+//     1/nv = chi nu nv^2 w^2 (t != 0), so 1/V = conj(V) / nv and gx1, x1 are affine,
+//     y1 = nu nv w: y1^2 = chi norm(gx1), i.e. sqrt(norm gx1) when chi = 1;
+//   chi = -1: x2 = Z u^2 x1, gx2 = (Z u^2)^3 gx1, norm gx2 = 125 N(u)^6 norm gx1 (norm Z = 5), so
+//     sqrt(norm gx2) = sqrt(-125) N(u)^3 y1;
+//   then the complex method from alpha = sqrt(norm gx) (one more exponentiation), as fp2_sqrt_p.
+template <class Pow>
+LB_HD g2j map_to_curve_g2_fold(const fp2& u, Pow pow) {
+  const fp2 A = fp2_load(LB_SSWU_A), B = fp2_load(LB_SSWU_B), Z = fp2_load(LB_SSWU_Z);
+  const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
+  const fp2 tv1 = fp2_add(fp2_sqr(zu2), zu2);
+  const bool exc = fp2_is_zero(tv1);
+  // x1 = -B (1 + 1/tv1) / A = -B (tv1 + 1) / (A tv1); tv1 = 0: B / (Z A)
+  const fp2 N = fp2_select(exc, B, fp2_neg(fp2_mul(B, fp2_add(tv1, fp2_one()))));
+  const fp2 D = fp2_select(exc, fp2_mul(Z, A), fp2_mul(A, tv1));
+  const fp2 D2 = fp2_sqr(D), V = fp2_mul(D2, D);
+  const fp2 U = fp2_add(fp2_mul(fp2_add(fp2_sqr(N), fp2_mul(A, D2)), N), fp2_mul(B, V));
+  const fp nu = fp_add(fp_sqr(U.c0), fp_sqr(U.c1)), nv = fp_add(fp_sqr(V.c0), fp_sqr(V.c1));
+  const fp nv2 = fp_sqr(nv);
+  const fp t = fp_mul(nu, fp_mul(nv2, nv));
+  const fp w = pow(t, LB_EXP_ISQRT, 378);
+  const fp w2 = fp_sqr(w);
+  const fp chi = fp_mul(w2, t);
+  const bool qr = !fp_eq(chi, fp_neg(fp_one()));  // chi = 1, or 0 (gx1 = 0 is a square)
+  fp inv_nv = fp_mul(fp_mul(nu, nv2), w2);
+  if (!qr) inv_nv = fp_neg(inv_nv);
+  if (fp_is_zero(nu)) inv_nv = fp_inv_i(nv);  // gx1 = 0 (V != 0: D != 0 always)
+  const fp2 inv_v = fp2_mul_fp(fp2_conj(V), inv_nv);
+  fp2 x = fp2_mul(fp2_mul(N, D2), inv_v);  // N / D
+  fp2 gx = fp2_mul(U, inv_v);
+  fp alpha = fp_mul(fp_mul(nu, nv), w);
+  if (!qr) {
+    const fp nuu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
+    alpha = fp_mul(alpha, fp_mul(fp_load(LB_SQRT_M125), fp_mul(fp_sqr(nuu), nuu)));
+    x = fp2_mul(zu2, x);
+    gx = fp2_mul(gx, fp2_mul(fp2_sqr(zu2), zu2));
+  }
+  // complex method (fp2_sqrt_i) from alpha
+  const fp inv2 = fp_load(LB_INV2);
+  const fp d1 = fp_mul(fp_add(gx.c0, alpha), inv2);
+  const fp d2 = fp_mul(fp_sub(gx.c0, alpha), inv2);
+  const fp delta = fp_select(fp_is_zero(d1), d2, d1);
+  const fp z = pow(delta, LB_EXP_ISQRT, 378);
+  const fp s = fp_mul(delta, z);
+  const bool delta_qr = fp_eq(fp_sqr(s), delta);
+  fp tt = fp_mul(z, inv2);
+  if (!delta_qr) tt = fp_neg(tt);
+  const fp q = fp_mul(gx.c1, tt);
+  fp2 y{fp_select(delta_qr, s, q), fp_select(delta_qr, q, s)};
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  // 3-isogeny E2' -> E2 (as map_to_curve_g2)
+  const fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
+  const fp2 xn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_XNUM3), xxx), fp2_mul(fp2_load(LB_ISO_XNUM2), xx)),
+                                 fp2_mul(fp2_load(LB_ISO_XNUM1), x)),
+                         fp2_load(LB_ISO_XNUM0));
+  const fp2 xd = fp2_add(fp2_add(xx, fp2_mul(fp2_load(LB_ISO_XDEN1), x)), fp2_load(LB_ISO_XDEN0));
+  const fp2 yn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_YNUM3), xxx), fp2_mul(fp2_load(LB_ISO_YNUM2), xx)),
+                                 fp2_mul(fp2_load(LB_ISO_YNUM1), x)),
+                         fp2_load(LB_ISO_YNUM0));
+  const fp2 yd = fp2_add(fp2_add(fp2_add(xxx, fp2_mul(fp2_load(LB_ISO_YDEN2), xx)), fp2_mul(fp2_load(LB_ISO_YDEN1), x)),
+                         fp2_load(LB_ISO_YDEN0));
+  g2j r;
+  const fp2 yd2 = fp2_sqr(yd);
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
+  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(fp2_sqr(xd), xd)), yd2);
+  return r;
+}
+
 // hash_to_G2(msg32) in Jacobian coordinates (RFC 9380 §3 hash_to_curve)
 LB_HD g2j hash_to_g2(const uint8_t msg[32]) {
   uint32_t ub[64];

@@ -570,7 +570,7 @@ __global__ void __launch_bounds__(64) k_decompress_sigs_row(uint32_t n, const ui
                                                             uint32_t* __restrict__ sig_aff, uint4* __restrict__ sig_aos,
                                                             uint32_t* __restrict__ sig_inf,
                                                             int32_t* __restrict__ sig_status) {
-  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 4;
+  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> (LB_H2C_FOLD ? 5 : 4);  // a row pair (r2_pow_const) / a row
   const uint32_t ic = i < n ? i : n - 1;  // rows past the end decode the last signature again
   int st = LB_OK;
   g2a a;
@@ -586,9 +586,13 @@ __global__ void __launch_bounds__(64) k_decompress_sigs_row(uint32_t n, const ui
       const uint4 v = s[k];
       w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
     }
+#if LB_H2C_FOLD
+    st = g2_decompress96_wp(w, a, inf, [](const fp& x, const uint32_t* e, int top) { return r2_pow_const(x, e, top); });
+#else
     st = g2_decompress96_wp(w, a, inf, [](const fp& x, const uint32_t* e, int top) { return r1_pow_const(x, e, top); });
+#endif
   }
-  if (i >= n || (threadIdx.x & 15) != 0) return;
+  if (i >= n || (threadIdx.x & (LB_H2C_FOLD ? 31 : 15)) != 0) return;
   soa_st(sig_aff, n, i, a);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
   LB_UNROLL for (int k = 0; k < 12; k++) sig_aos[(size_t)12 * i + k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
@@ -602,6 +606,24 @@ __global__ void __launch_bounds__(64) k_decompress_sigs_row(uint32_t n, const ui
 #if LB_KG(13)
 __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, const uint32_t* __restrict__ uniq_set,
                                                      const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
+#if LB_H2C_FOLD
+  // two items per wave, a row PAIR each (r2_pow_const), map_to_curve_g2_fold
+  const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 5;
+  if (blockIdx.x * 2 >= 2 * nu) return;  // (whole wave)
+  const uint32_t tc = t < 2 * nu ? t : 2 * nu - 1;
+  const uint32_t which = tc < nu ? 0u : 1u;
+  const uint32_t u = which ? tc - nu : tc;
+  const uint4* m4 = reinterpret_cast<const uint4*>(msgs + (size_t)32 * uniq_set[u]);
+  uint32_t M[8];
+  LB_UNROLL for (int i = 0; i < 2; i++) {
+    const uint4 v = m4[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    LB_UNROLL for (int k = 0; k < 4; k++) M[4 * i + k] = __builtin_bswap32(w[k]);
+  }
+  const g2j r = map_to_curve_g2_fold(hash_to_field_u(M, (int)which),
+                                     [](const fp& a, const uint32_t* e, int top) { return r2_pow_const(a, e, top); });
+  if (t < 2 * nu && (threadIdx.x & 31) == 0) soa_st(q, 2 * n, which * n + u, r);
+#else
   const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 4;
   if (blockIdx.x * 4 >= 2 * nu) return;  // (whole wave)
   const uint32_t tc = t < 2 * nu ? t : 2 * nu - 1;  // rows past the end recompute the last item
@@ -616,6 +638,7 @@ __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, co
   }
   const g2j r = map_to_curve_g2_i<true>(hash_to_field_u(M, (int)which));
   if (t < 2 * nu && (threadIdx.x & 15) == 0) soa_st(q, 2 * n, which * n + u, r);
+#endif
 }
 #endif  // LB_KG
 

@@ -804,6 +804,34 @@ __device__ fp r1_pow_const(const fp& a, const uint32_t* e, int top_bit) {
   return r1_export(r, k);
 }
 
+// An Fp exponentiation by a constant on a PAIR of rows (rows 2j, 2j + 1 of a wave; every lane of
+// both rows holds the same fp): right to left, the even row squares (s = a^(2^i)) while the odd
+// row multiplies its accumulator by the same s when bit i is set, in the same row product; then
+// the even row's new s moves to the odd row (v_permlane16_swap, a VALU op).  The chain is one
+// product per exponent bit (378 for (p-3)/4) against r1_pow_const's squarings plus one product
+// per 4-bit window (~460).
+__device__ __forceinline__ fp r2_pow_const(const fp& a, const uint32_t* e, int top_bit) {
+  const int k = r_limb();
+  const bool odd = (threadIdx.x >> 4) & 1;
+  int s = r1_import(a, k);
+  int acc = r1_import(fp_one(), k);
+  for (int i = 0; i <= top_bit; i++) {
+    const bool b = (e[i >> 5] >> (i & 31)) & 1u;  // uniform
+    int x[14];
+    r_rep(s, x);
+    const int r = rp_mul(x, odd ? acc : s, k);
+    const int even_r = __builtin_amdgcn_permlane16_swap(r, r, false, false)[0];  // odd rows: the even row's r
+    if (odd) {
+      if (b) acc = r;
+      s = even_r;
+    } else {
+      s = r;
+    }
+  }
+  const int odd_acc = __builtin_amdgcn_permlane16_swap(acc, acc, false, false)[1];  // even rows: the odd row's acc
+  return r1_export(odd ? acc : odd_acc, k);
+}
+
 // ---------------------------------------------------------------- op lists (one r_exec site)
 // A fixed sequence of Fp12 / G2 / Miller-step operations as a table of (kind, dst, a, b) words
 // built at compile time (constexpr), run by r_run: one loop with the interpreter inlined once, so

@@ -35,6 +35,9 @@ void h_hash_to_field(const uint8_t* msg, uint8_t* out192) {
   for (int k = 0; k < 4; k++) wr(out192 + 48 * k, fp_from_be64_words(ub + 16 * k));
 }
 int h_map_to_curve(const uint8_t* u96, uint8_t* out192) { return wrg2(out192, map_to_curve_g2(rd2(u96))); }
+int h_map_to_curve_fold(const uint8_t* u96, uint8_t* out192) {
+  return wrg2(out192, map_to_curve_g2_fold(rd2(u96), [](const fp& a, const uint32_t* e, int top) { return fp_pow_const(a, e, top); }));
+}
 int h_hash_to_g2(const uint8_t* msg, uint8_t* out192) { return wrg2(out192, hash_to_g2(msg)); }
 int h_g2_clear_cofactor(const uint8_t* p192, uint8_t* out192) { return wrg2(out192, g2_clear_cofactor(jac_from_aff(rdg2(p192)))); }
 int h_g2_in_subgroup(const uint8_t* p192) { return g2_in_subgroup(jac_from_aff(rdg2(p192))); }

@@ -120,6 +120,32 @@ def test_hash_to_g2_stages(L):
         assert fg2(o192.raw) == o.hash_to_g2(msg)
 
 
+def test_map_to_curve_fold(L):
+    # map_to_curve_g2_fold (the Legendre symbol and the inversion folded into the square root's
+    # first exponentiation; k_hash_map_row) against the oracle's SSWU + 3-isogeny: random field
+    # elements (both branches of the square test), hash_to_field outputs, u = 0 (tv1 = 0)
+    rnd = random.Random(11)
+    us = [(rnd.randrange(P), rnd.randrange(P)) for _ in range(24)] + [(0, 0), (1, 0), (0, 1), (P - 1, 0)]
+    for msg in [bytes(32), bytes(range(32))]:
+        us += list(o.hash_to_field_fp2(msg, 2, o.DST_POP))
+    branches = set()
+    o192 = buf(192)
+    for ui in us:
+        assert L.h_map_to_curve_fold(b2(ui), o192)
+        assert fg2(o192.raw) == o.iso_map(o.map_to_curve_sswu(ui))
+        L.h_map_to_curve(b2(ui), o192)
+        assert fg2(o192.raw) == o.iso_map(o.map_to_curve_sswu(ui))
+        zu2 = o.f2_mul(o.SSWU_Z, o.f2_sqr(ui))
+        tv1 = o.f2_add(o.f2_sqr(zu2), zu2)
+        if o.f2_is_zero(tv1):
+            x1 = o.f2_mul(o.SSWU_B, o.f2_inv(o.f2_mul(o.SSWU_Z, o.SSWU_A)))
+        else:
+            x1 = o.f2_mul(o.f2_mul(o.f2_neg(o.SSWU_B), o.f2_inv(o.SSWU_A)), o.f2_add(o.F2_ONE, o.f2_inv(tv1)))
+        gx1 = o.f2_add(o.f2_add(o.f2_mul(o.f2_sqr(x1), x1), o.f2_mul(o.SSWU_A, x1)), o.SSWU_B)
+        branches.add(o.f2_is_square(gx1))
+    assert branches == {True, False}
+
+
 def test_g2_subgroup_cofactor_psi(L):
     msg = bytes(range(32))
     H = o.hash_to_g2(msg)
