@@ -139,6 +139,9 @@ struct lb_engine {
   uint32_t prio_max = 0;
   hipEvent_t ev_g1 = nullptr, ev_s = nullptr, ev_fork = nullptr, ev_dec = nullptr, ev_pk = nullptr;
   hipEvent_t ev_pkst = nullptr;  // the pubkey statuses (k_pk_blind mode 1), before the ladder
+  // small batches alone (round 6): the decoded signatures (s2) -> r_i sig_i on s3 beside the
+  // subgroup check (ev_sdec), and the terms ready for the sum on s2 (ev_sblind)
+  hipEvent_t ev_sdec = nullptr, ev_sblind = nullptr;
   std::mutex mu;
   // workspace
   dbuf scalars, sig_aff, sig_inf, sig_status, q, h_aff, rpk, rsig, pk_status, ml, treeP, treeS, job_status,
@@ -206,6 +209,9 @@ struct lb_engine {
   // round 6: the row forms' G2 chains (cofactor clearing, the subgroup ladder, r_i sig_i) in
   // projective coordinates with the complete formulas; LB_ROW_PROJ=0: the Jacobian programs
   bool row_proj = true;
+  // round 6, small batches alone: the r PK ladder on rows and r_i sig_i on s3 beside the
+  // subgroup check; LB_SMALL_PAR=0: both on their round-5 streams and forms (A/B)
+  bool small_par = true;
   // ... and the signature decode's square roots on rows up to this many sets.  LB_DEC_ROW_MAX.
   uint32_t dec_row_max = 4096;
   // ... and the signatures' subgroup check with 8 lanes per set (k_sig_subgroup_g8).  LB_SUBGROUP_G8_MAX.
@@ -460,6 +466,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   if (const char* dr = getenv("LB_DEC_ROW_MAX")) e->dec_row_max = (uint32_t)strtoul(dr, nullptr, 10);
   if (const char* hc = getenv("LB_HASH_ROW_CAREFUL")) e->hash_row_careful = (uint32_t)strtoul(hc, nullptr, 10);
   if (const char* rp = getenv("LB_ROW_PROJ")) e->row_proj = std::atoi(rp) != 0;
+  if (const char* sp = getenv("LB_SMALL_PAR")) e->small_par = std::atoi(sp) != 0;
   if (const char* sg = getenv("LB_SUBGROUP_G8_MAX")) e->subgroup_g8_max = (uint32_t)strtoul(sg, nullptr, 10);
   if (const char* ss = getenv("LB_SMALL_S_MAX")) e->small_s_max = (uint32_t)strtoul(ss, nullptr, 10);
   if (const char* sg8 = getenv("LB_SMALL_S_G8_MAX")) e->small_s_g8_max = (uint32_t)strtoul(sg8, nullptr, 10);
@@ -513,6 +520,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
                 : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
   };
   if (mk(&e->stream, true) != hipSuccess || mk(&e->stream2, false) != hipSuccess || mk(&e->stream3, false) != hipSuccess ||
+
       hipHostMalloc((void**)&e->h_nu, 8, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&e->h_flag, 4, hipHostMallocDefault) != hipSuccess) {
     if (e->stream) hipStreamDestroy(e->stream);
@@ -531,6 +539,8 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
   hipEventCreateWithFlags(&e->ev_dec, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_pk, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_pkst, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_sdec, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_sblind, hipEventDisableTiming);
   for (int i = 0; i < kStages; i++) {
     hipEventCreate(&e->ev0[i]);
     hipEventCreate(&e->ev1[i]);
@@ -563,6 +573,9 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
           hipLaunchKernelGGL(k_decompress_sigs, dim3(4096), dim3(LB_TPB), 0, e->stream2, 0u, nullptr, nullptr, nullptr,
                              nullptr, nullptr, nullptr);
           hipLaunchKernelGGL(k_pk_chunks, dim3(4096), dim3(LB_TPB), 0, e->stream3, 0u, nullptr, nullptr, nullptr, nullptr);
+          // the row r PK ladder (one row per set), at the largest small batch
+          hipLaunchKernelGGL(k_pk_blind_rowp, dim3(std::max<uint32_t>(1u, (e->row_max + 3) / 4)), dim3(64), 0, e->stream3,
+                             0u, nullptr, nullptr, nullptr, nullptr);
         }
         if (res23 >= 2) {
           // (one wave per 8 sets, at least one wave, at most 16 384: more than the device holds)
@@ -610,6 +623,8 @@ void lb_engine_destroy(lb_engine* e) {
   hipEventDestroy(e->ev_dec);
   hipEventDestroy(e->ev_pk);
   if (e->ev_pkst) hipEventDestroy(e->ev_pkst);
+  if (e->ev_sdec) hipEventDestroy(e->ev_sdec);
+  if (e->ev_sblind) hipEventDestroy(e->ev_sblind);
   hipStreamSynchronize(e->stream2);
   hipStreamSynchronize(e->stream3);
   if (e->scratch) delete e->scratch;
@@ -1103,6 +1118,13 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     // on its own stream the pubkey side splits: the aggregates' statuses (what the job statuses
     // and so the S side need) first, then the r PK ladder (only the per-root sums need it)
     const bool pk_split = s3 != s2;
+    // small batches alone: the r PK ladder (k_pk_blind mode 2) with row products, one 16-lane row
+    // per set (on s3, before r_i sig_i; a fourth stream per engine, round 6, put 7 engines' 28
+    // streams past what the device schedules without stalls: +10 ms on some batches)
+    const bool pk_rowp = e->small_par && pk_split && !e->straus_run && n <= e->row_max && e->alone && e->row_fe;
+    // r_i sig_i on s3 beside the subgroup check (small batches alone, row forms, one-workgroup sum)
+    const bool sb_par = e->small_par && pk_split && !one_unblinded && n <= e->small_s_max && n <= e->small_s_g8_max &&
+                        n <= e->row_max && e->alone && e->row_fe && !e->straus_run;
     {
       stage_scope sc(e, ST_PK_BLIND, s3);
       // modes: 0 all, 1 aggregate + status (+ pk3 for the Straus sums), 2 the per-set ladder
@@ -1110,6 +1132,11 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       const uint32_t m1 = e->straus_run ? 1u : (pk_split ? 2u : 0u);
       if (e->straus_run) LB_HIP(e->pk3.ensure((size_t)ns * sizeof(g1x3)));
       for (uint32_t mode = m0; mode <= m1; mode++) {
+        if (mode == 2u && pk_rowp) {
+          hipLaunchKernelGGL(k_pk_blind_rowp, dim3((n + 3) / 4), dim3(64), 0, s3, n, e->pk_aff.as<uint32_t>(),
+                             e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
+          continue;
+        }
         hipLaunchKernelGGL(k_pk_blind, dim3(nblk_inv(n)), dim3(LB_INV_TPB), 0, s3, n, nc, b->d_set_chunk_off.as<uint32_t>(),
                            e->chunk_acc.as<uint32_t>(), e->chunk_status.as<int32_t>(), e->pk_aff.as<uint32_t>(),
                            e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>(), mode,
@@ -1129,6 +1156,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         hipLaunchKernelGGL(k_decompress_sigs, dim3(nblk(n)), dim3(LB_TPB), 0, s2, n, b->d_sigs.as<uint8_t>(),
                            b->has_sizes ? b->d_sig_sizes.as<uint32_t>() : nullptr, e->sig_aff.as<uint32_t>(),
                            e->sig_aos.as<uint4>(), e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      if (sb_par) LB_HIP(hipEventRecord(e->ev_sdec, s2));
       // (8 lanes per signature also for a slot while the device is otherwise idle ran slower:
       // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
       if (n <= e->row_max && e->alone && e->row_fe)
@@ -1146,6 +1174,20 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                          e->set_live.as<uint32_t>());
     }
     LB_HIP(hipEventRecord(e->ev_dec, s2));
+    if (sb_par) {
+      // r_i sig_i of every decoded set on s3 (after its pubkey work) beside s2's subgroup check and
+      // job statuses; the sum on s2 masks the terms by liveness
+      LB_HIP(hipStreamWaitEvent(s3, e->ev_sdec, 0));
+      if (e->profiling) {
+        hipEventRecord(e->ev0[ST_SIG_MSM], s3);
+        e->used[ST_SIG_MSM] = true;
+      }
+      LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
+      hipLaunchKernelGGL(k_sig_blind_row, dim3(n), dim3(LBR_NT), 0, s3, n, e->sig_aff.as<uint32_t>(),
+                         e->scalars.as<uint64_t>(), nullptr, e->sig_inf.as<uint32_t>(), e->s_terms.as<uint32_t>(),
+                         e->row_proj ? 1u : 0u);
+      LB_HIP(hipEventRecord(e->ev_sblind, s3));
+    }
     // ---- s1: group the sets by signing root
     {
       stage_scope sc(e, ST_DEDUP, s1);
@@ -1164,12 +1206,37 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         if (e->root_shuffle)
           hipLaunchKernelGGL(k_msg_uid, dim3(nblk(cap)), dim3(LB_TPB), 0, s1, cap, e->msg_tab.as<uint32_t>(),
                              e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
-        else
-          hipLaunchKernelGGL(k_msg_uid_input, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
-                             e->uid_of.as<uint32_t>(), e->uniq_set.as<uint32_t>(), e->n_u.as<uint32_t>());
-        hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
-                           e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
-                           e->gpos.as<uint32_t>());
+        else {
+          // input order (LB_ROOT_SHUFFLE=0: A/B and the search-trace tests), made deterministic on
+          // the host: roots numbered by first occurrence and members in input order within a root
+          // (the device form's atomics order both by wave scheduling, so two runs of one batch
+          // could build different root trees)
+          std::vector<uint32_t> rep(n), uid(n, 0xffffffffu), uniq, suid(n), cnt, pos(n);
+          LB_HIP(hipMemcpyAsync(rep.data(), e->rep_of.p, (size_t)n * 4, hipMemcpyDeviceToHost, s1));
+          LB_HIP(hipStreamSynchronize(s1));
+          for (uint32_t i = 0; i < n; i++) {
+            const uint32_t r = rep[i];
+            if (uid[r] == 0xffffffffu) {
+              uid[r] = (uint32_t)uniq.size();
+              uniq.push_back(r);
+              cnt.push_back(0);
+            }
+            suid[i] = uid[r];
+            pos[i] = cnt[uid[r]]++;
+          }
+          const uint32_t nun = (uint32_t)uniq.size();
+          LB_HIP(hipMemcpyAsync(e->uid_of.p, uid.data(), (size_t)n * 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipMemcpyAsync(e->uniq_set.p, uniq.data(), (size_t)nun * 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipMemcpyAsync(e->set_uid.p, suid.data(), (size_t)n * 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipMemcpyAsync(e->gcnt.p, cnt.data(), (size_t)nun * 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipMemcpyAsync(e->gpos.p, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipMemcpyAsync(e->n_u.p, &nun, 4, hipMemcpyHostToDevice, s1));
+          LB_HIP(hipStreamSynchronize(s1));
+        }
+        if (e->root_shuffle)
+          hipLaunchKernelGGL(k_msg_count, dim3(nblk(n)), dim3(LB_TPB), 0, s1, n, e->rep_of.as<uint32_t>(),
+                             e->uid_of.as<uint32_t>(), e->set_uid.as<uint32_t>(), e->gcnt.as<uint32_t>(),
+                             e->gpos.as<uint32_t>());
         hipLaunchKernelGGL(k_msg_scan, dim3(1), dim3(1024), 0, s1, nu, 0u, e->gchunk, e->gcnt.as<uint32_t>(), e->goff.as<uint32_t>(),
                            e->gch.as<uint32_t>(), nullptr, nullptr, nullptr, e->n_u.as<uint32_t>() + 1);
         hipLaunchKernelGGL(k_chunk_fill, dim3(nblk(n + n / e->gchunk + 1)), dim3(LB_TPB), 0, s1, nu,
@@ -1224,7 +1291,12 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       }
     }
     // ---- s2: S = sum r_i sig_i by bucket MSM, overlapped with the Miller loops
-    if (one_unblinded) {
+    if (sb_par) {
+      LB_HIP(hipStreamWaitEvent(s2, e->ev_sblind, 0));
+      hipLaunchKernelGGL(k_g2_sum_g8, dim3(1), dim3(8 * LB_SUM_G8_GROUPS), 0, s2, n, e->s_terms.as<uint32_t>(),
+                         2 * mj, e->treeS.as<uint32_t>(), 1u, e->set_live.as<uint32_t>());
+      if (e->profiling) hipEventRecord(e->ev1[ST_SIG_MSM], s2);
+    } else if (one_unblinded) {
       stage_scope sc(e, ST_SIG_MSM, s2);
       hipLaunchKernelGGL(k_sig_unblinded, dim3(1), dim3(64), 0, s2, e->sig_aff.as<uint32_t>(),
                          e->set_live.as<uint32_t>(), e->sig_inf.as<uint32_t>(), 2 * mj, e->treeS.as<uint32_t>());
@@ -1246,7 +1318,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
                            e->s_terms.as<uint32_t>());
       if (n <= e->small_s_g8_max) {  // one workgroup of 8-lane additions
         hipLaunchKernelGGL(k_g2_sum_g8, dim3(1), dim3(8 * LB_SUM_G8_GROUPS), 0, s2, n, e->s_terms.as<uint32_t>(),
-                           2 * mj, e->treeS.as<uint32_t>(), 1u);
+                           2 * mj, e->treeS.as<uint32_t>(), 1u, nullptr);
       } else {
         // 64:1 levels, ping-ponging between the two buffers; the last level writes treeS[1]
         uint32_t* bufs[2] = {e->s_terms.as<uint32_t>(), e->s_part.as<uint32_t>()};

@@ -210,67 +210,88 @@ LB_NI g2j map_to_curve_g2(fp2 u) {
 //   chi = -1: x2 = Z u^2 x1, gx2 = (Z u^2)^3 gx1, norm gx2 = 125 N(u)^6 norm gx1 (norm Z = 5), so
 //     sqrt(norm gx2) = sqrt(-125) N(u)^3 y1;
 //   then the complex method from alpha = sqrt(norm gx) (one more exponentiation), as fp2_sqrt_p.
-template <class Pow>
-LB_HD g2j map_to_curve_g2_fold(const fp2& u, Pow pow) {
-  const fp2 A = fp2_load(LB_SSWU_A), B = fp2_load(LB_SSWU_B), Z = fp2_load(LB_SSWU_Z);
-  const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
-  const fp2 tv1 = fp2_add(fp2_sqr(zu2), zu2);
-  const bool exc = fp2_is_zero(tv1);
+// Generic over the field types (F2, F): fp2 / fp (lane arithmetic, the CPU harness) or rfp2 / rfp
+// (lb_row.h: every product a row product, k_hash_map_row), through f_* and the fl_* policy below;
+// pow: F -> F.  Decisions and the output go through canonical values (fl_out).
+LB_HD fp fl_in(const fp& a, const fp*) { return a; }
+LB_HD fp2 fl_in(const fp2& a, const fp2*) { return a; }
+LB_HD fp fl_out(const fp& a) { return a; }
+LB_HD fp2 fl_out(const fp2& a) { return a; }
+LB_HD fp fl_norm(const fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+LB_HD fp2 fl_mulb(const fp2& a, const fp& s) { return fp2_mul_fp(a, s); }
+LB_HD fp2 fl_conj(const fp2& a) { return fp2_conj(a); }
+LB_HD fp2 fl_make(const fp& a, const fp& b) { return fp2{a, b}; }
+LB_HD fp fl_c0(const fp2& a) { return a.c0; }
+LB_HD fp fl_c1(const fp2& a) { return a.c1; }
+template <class F2, class F, class Pow>
+LB_HD g2j map_to_curve_g2_fold_t(const fp2& u_in, Pow pow) {
+  const F2* t2 = nullptr;
+  const F* t1 = nullptr;
+  auto C2 = [&](const uint32_t* c) { return fl_in(fp2_load(c), t2); };
+  const F2 u = fl_in(u_in, t2);
+  const F2 A = C2(LB_SSWU_A), B = C2(LB_SSWU_B), Z = C2(LB_SSWU_Z);
+  const F2 zu2 = f_mul(Z, f_sqr(u));
+  const F2 tv1 = f_add(f_sqr(zu2), zu2);
+  const bool exc = fp2_is_zero(fl_out(tv1));
+  F2 one;
+  f_set_one(one);
   // x1 = -B (1 + 1/tv1) / A = -B (tv1 + 1) / (A tv1); tv1 = 0: B / (Z A)
-  const fp2 N = fp2_select(exc, B, fp2_neg(fp2_mul(B, fp2_add(tv1, fp2_one()))));
-  const fp2 D = fp2_select(exc, fp2_mul(Z, A), fp2_mul(A, tv1));
-  const fp2 D2 = fp2_sqr(D), V = fp2_mul(D2, D);
-  const fp2 U = fp2_add(fp2_mul(fp2_add(fp2_sqr(N), fp2_mul(A, D2)), N), fp2_mul(B, V));
-  const fp nu = fp_add(fp_sqr(U.c0), fp_sqr(U.c1)), nv = fp_add(fp_sqr(V.c0), fp_sqr(V.c1));
-  const fp nv2 = fp_sqr(nv);
-  const fp t = fp_mul(nu, fp_mul(nv2, nv));
-  const fp w = pow(t, LB_EXP_ISQRT, 378);
-  const fp w2 = fp_sqr(w);
-  const fp chi = fp_mul(w2, t);
+  const F2 N = f_select(exc, B, f_neg(f_mul(B, f_add(tv1, one))));
+  const F2 D = f_select(exc, f_mul(Z, A), f_mul(A, tv1));
+  const F2 D2 = f_sqr(D), V = f_mul(D2, D);
+  const F2 U = f_add(f_mul(f_add(f_sqr(N), f_mul(A, D2)), N), f_mul(B, V));
+  const F nu = fl_norm(U), nv = fl_norm(V);
+  const F nv2 = f_sqr(nv);
+  const F t = f_mul(nu, f_mul(nv2, nv));
+  const F w = pow(t, LB_EXP_ISQRT, 378);
+  const F w2 = f_sqr(w);
+  const fp chi = fl_out(f_mul(w2, t));
   const bool qr = !fp_eq(chi, fp_neg(fp_one()));  // chi = 1, or 0 (gx1 = 0 is a square)
-  fp inv_nv = fp_mul(fp_mul(nu, nv2), w2);
-  if (!qr) inv_nv = fp_neg(inv_nv);
-  if (fp_is_zero(nu)) inv_nv = fp_inv_i(nv);  // gx1 = 0 (V != 0: D != 0 always)
-  const fp2 inv_v = fp2_mul_fp(fp2_conj(V), inv_nv);
-  fp2 x = fp2_mul(fp2_mul(N, D2), inv_v);  // N / D
-  fp2 gx = fp2_mul(U, inv_v);
-  fp alpha = fp_mul(fp_mul(nu, nv), w);
+  F inv_nv = f_mul(f_mul(nu, nv2), w2);
+  if (!qr) inv_nv = f_neg(inv_nv);
+  if (fp_is_zero(chi)) inv_nv = fl_in(fp_inv_i(fl_out(nv)), t1);  // gx1 = 0 (V != 0: D != 0 always)
+  const F2 inv_v = fl_mulb(fl_conj(V), inv_nv);
+  F2 x = f_mul(f_mul(N, D2), inv_v);  // N / D
+  F2 gx = f_mul(U, inv_v);
+  F alpha = f_mul(f_mul(nu, nv), w);
   if (!qr) {
-    const fp nuu = fp_add(fp_sqr(u.c0), fp_sqr(u.c1));
-    alpha = fp_mul(alpha, fp_mul(fp_load(LB_SQRT_M125), fp_mul(fp_sqr(nuu), nuu)));
-    x = fp2_mul(zu2, x);
-    gx = fp2_mul(gx, fp2_mul(fp2_sqr(zu2), zu2));
+    const F nuu = fl_norm(u);
+    alpha = f_mul(alpha, f_mul(fl_in(fp_load(LB_SQRT_M125), t1), f_mul(f_sqr(nuu), nuu)));
+    x = f_mul(zu2, x);
+    gx = f_mul(gx, f_mul(f_sqr(zu2), zu2));
   }
   // complex method (fp2_sqrt_i) from alpha
-  const fp inv2 = fp_load(LB_INV2);
-  const fp d1 = fp_mul(fp_add(gx.c0, alpha), inv2);
-  const fp d2 = fp_mul(fp_sub(gx.c0, alpha), inv2);
-  const fp delta = fp_select(fp_is_zero(d1), d2, d1);
-  const fp z = pow(delta, LB_EXP_ISQRT, 378);
-  const fp s = fp_mul(delta, z);
-  const bool delta_qr = fp_eq(fp_sqr(s), delta);
-  fp tt = fp_mul(z, inv2);
-  if (!delta_qr) tt = fp_neg(tt);
-  const fp q = fp_mul(gx.c1, tt);
-  fp2 y{fp_select(delta_qr, s, q), fp_select(delta_qr, q, s)};
-  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  const F inv2 = fl_in(fp_load(LB_INV2), t1);
+  const F g0 = fl_c0(gx);
+  const F d1 = f_mul(f_add(g0, alpha), inv2);
+  const F d2 = f_mul(f_sub(g0, alpha), inv2);
+  const F delta = f_select(fp_is_zero(fl_out(d1)), d2, d1);
+  const F z = pow(delta, LB_EXP_ISQRT, 378);
+  const F s = f_mul(delta, z);
+  const bool delta_qr = f_eq(f_sqr(s), delta);
+  F tt = f_mul(z, inv2);
+  if (!delta_qr) tt = f_neg(tt);
+  const F q = f_mul(fl_c1(gx), tt);
+  F2 y = fl_make(f_select(delta_qr, s, q), f_select(delta_qr, q, s));
+  if (fp2_sgn0(u_in) != fp2_sgn0(fl_out(y))) y = f_neg(y);
   // 3-isogeny E2' -> E2 (as map_to_curve_g2)
-  const fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
-  const fp2 xn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_XNUM3), xxx), fp2_mul(fp2_load(LB_ISO_XNUM2), xx)),
-                                 fp2_mul(fp2_load(LB_ISO_XNUM1), x)),
-                         fp2_load(LB_ISO_XNUM0));
-  const fp2 xd = fp2_add(fp2_add(xx, fp2_mul(fp2_load(LB_ISO_XDEN1), x)), fp2_load(LB_ISO_XDEN0));
-  const fp2 yn = fp2_add(fp2_add(fp2_add(fp2_mul(fp2_load(LB_ISO_YNUM3), xxx), fp2_mul(fp2_load(LB_ISO_YNUM2), xx)),
-                                 fp2_mul(fp2_load(LB_ISO_YNUM1), x)),
-                         fp2_load(LB_ISO_YNUM0));
-  const fp2 yd = fp2_add(fp2_add(fp2_add(xxx, fp2_mul(fp2_load(LB_ISO_YDEN2), xx)), fp2_mul(fp2_load(LB_ISO_YDEN1), x)),
-                         fp2_load(LB_ISO_YDEN0));
+  const F2 xx = f_sqr(x), xxx = f_mul(xx, x);
+  const F2 xn = f_add(f_add(f_add(f_mul(C2(LB_ISO_XNUM3), xxx), f_mul(C2(LB_ISO_XNUM2), xx)), f_mul(C2(LB_ISO_XNUM1), x)),
+                      C2(LB_ISO_XNUM0));
+  const F2 xd = f_add(f_add(xx, f_mul(C2(LB_ISO_XDEN1), x)), C2(LB_ISO_XDEN0));
+  const F2 yn = f_add(f_add(f_add(f_mul(C2(LB_ISO_YNUM3), xxx), f_mul(C2(LB_ISO_YNUM2), xx)), f_mul(C2(LB_ISO_YNUM1), x)),
+                      C2(LB_ISO_YNUM0));
+  const F2 yd = f_add(f_add(f_add(xxx, f_mul(C2(LB_ISO_YDEN2), xx)), f_mul(C2(LB_ISO_YDEN1), x)), C2(LB_ISO_YDEN0));
+  const F2 yd2 = f_sqr(yd);
   g2j r;
-  const fp2 yd2 = fp2_sqr(yd);
-  r.z = fp2_mul(xd, yd);
-  r.x = fp2_mul(fp2_mul(xn, xd), yd2);
-  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), fp2_mul(fp2_sqr(xd), xd)), yd2);
+  r.z = fl_out(f_mul(xd, yd));
+  r.x = fl_out(f_mul(f_mul(xn, xd), yd2));
+  r.y = fl_out(f_mul(f_mul(f_mul(y, yn), f_mul(f_sqr(xd), xd)), yd2));
   return r;
+}
+template <class Pow>
+LB_HD g2j map_to_curve_g2_fold(const fp2& u, Pow pow) {
+  return map_to_curve_g2_fold_t<fp2, fp>(u, pow);
 }
 
 // hash_to_G2(msg32) in Jacobian coordinates (RFC 9380 §3 hash_to_curve)

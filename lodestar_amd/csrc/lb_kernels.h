@@ -607,7 +607,8 @@ __global__ void __launch_bounds__(64) k_decompress_sigs_row(uint32_t n, const ui
 __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, const uint32_t* __restrict__ uniq_set,
                                                      const uint8_t* __restrict__ msgs, uint32_t* __restrict__ q) {
 #if LB_H2C_FOLD
-  // two items per wave, a row PAIR each (r2_pow_const), map_to_curve_g2_fold
+  // two items per wave, a row PAIR each: map_to_curve_g2_fold with row products (rfp2 / rfp) and
+  // the exponentiations on the pair (r2_pow_rf)
   const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 5;
   if (blockIdx.x * 2 >= 2 * nu) return;  // (whole wave)
   const uint32_t tc = t < 2 * nu ? t : 2 * nu - 1;
@@ -620,8 +621,8 @@ __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, co
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     LB_UNROLL for (int k = 0; k < 4; k++) M[4 * i + k] = __builtin_bswap32(w[k]);
   }
-  const g2j r = map_to_curve_g2_fold(hash_to_field_u(M, (int)which),
-                                     [](const fp& a, const uint32_t* e, int top) { return r2_pow_const(a, e, top); });
+  const g2j r = map_to_curve_g2_fold_t<rfp2, rfp>(hash_to_field_u(M, (int)which),
+                                                [](const rfp& a, const uint32_t* e, int top) { return r2_pow_rf(a, e, top); });
   if (t < 2 * nu && (threadIdx.x & 31) == 0) soa_st(q, 2 * n, which * n + u, r);
 #else
   const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 4;
@@ -1154,6 +1155,67 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 }
 #endif  // LB_KG
 
+// k_pk_blind's mode 2 (the r PK ladder, from mode 1's pk_status / pk_aff) with one 16-lane row per
+// set, 4 sets per wave, every product a row product (lb_row.h rfp: the same generic GLV ladder,
+// jac_mul_glv_i<rfp>), for small batches on a device running alone: a C2 block's ladders are
+// ~600 serial lone-lane products each (~0.9 ms), here row products (~0.45 us each).
+#if LB_KG(13)
+__global__ void __launch_bounds__(64) k_pk_blind_rowp(uint32_t n, const uint32_t* __restrict__ pk_aff,
+                                                     const uint64_t* __restrict__ scalars, uint32_t* __restrict__ rpk,
+                                                     const int32_t* __restrict__ pk_status) {
+  if (n == 0) return;  // (the scratch reservation's empty dispatch)
+  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 4;
+  const uint32_t ic = i < n ? i : n - 1;  // rows past the end redo the last set
+  const int st = pk_status[ic];
+  const uint64_t w = scalars[ic];
+  g1j rj = jac_infinity<fp>();
+  if (st == LB_OK) {
+    const g1a pk = soa_ld<g1a>(pk_aff, n, ic);
+    if (w == 1) {  // the unblinded 1-set call: r PK = PK, affine (Z = 1)
+      rj = g1j{pk.x, pk.y, fp_one()};
+    } else {
+      // t2 = [lambda]PK = (beta x, y), t3 = PK + t2 = (beta^2 x, -y), as k_pk_blind
+      const aff<rfp> t1 = rf_of(pk);
+      const aff<rfp> t2{f_mul(t1.x, rf_of(fp_load(LB_GLV_BETA))), t1.y};
+      const aff<rfp> t3{f_mul(t1.x, rf_of(fp_load(LB_GLV_BETA2))), f_neg(t1.y)};
+      // the ladder from the top non-zero digit with untested additions: PK is in G1 (prime order
+      // r) and not O, and the running scalar A + B lambda (0 <= A, B < 2^33, growing by doubling
+      // from the top digit) never equals +-(d0 + d1 lambda) for a digit d != 0 -- the lattice
+      // {(a, b): a + b lambda = 0 mod r} has no non-zero vector with |a|, |b| < 2^64 (reduced
+      // basis (x^2, 1), (-1, x^2 - 1)) -- so acc != +-T_d and acc != O at every addition
+      // (madd-2007-bl's exceptional cases)
+      const uint32_t k0 = (uint32_t)w, k1 = (uint32_t)(w >> 32);
+      auto digit = [&](int b) { return ((k0 >> b) & 1u) | (((k1 >> b) & 1u) << 1); };
+      int b = 31;
+      while (b > 0 && digit(b) == 0) b--;  // w != 0 (the engine's scalars are non-zero)
+      auto tab = [&](uint32_t d) { return d == 1u ? t1 : (d == 2u ? t2 : t3); };
+      jac<rfp> acc = jac_from_aff(tab(digit(b)));
+      for (b--; b >= 0; b--) {
+        acc = jac_dbl_i(acc);
+        const uint32_t d = digit(b);
+        if (d != 0u) {  // madd-2007-bl without the tests
+          const aff<rfp> q = tab(d);
+          const rfp Z1Z1 = f_sqr(acc.z);
+          const rfp H = f_sub(f_mul(q.x, Z1Z1), acc.x);
+          const rfp rr = f_dbl(f_sub(f_mul(f_mul(q.y, acc.z), Z1Z1), acc.y));
+          const rfp HH = f_sqr(H);
+          const rfp I = f_dbl(f_dbl(HH));
+          const rfp J = f_mul(H, I);
+          const rfp V = f_mul(acc.x, I);
+          jac<rfp> r;
+          r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+          r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(acc.y, J)));
+          r.z = f_sub(f_sub(f_sqr(f_add(acc.z, H)), Z1Z1), HH);
+          acc = r;
+        }
+      }
+      rj = rf_fp(acc);
+    }
+  }
+  if (i < n && (threadIdx.x & 15) == 0) aos_st(rpk, i, rj);
+}
+#endif  // LB_KG
+
 // ---------------------------------------------------------------- Miller loops
 // ML(P_u, H(m_u)) with P_u = sum of r_i PK_i over the live sets signing m_u (bilinearity:
 // prod_i e(r_i PK_i, H(m)) = e(sum_i r_i PK_i, H(m))), written straight into leaf m + u of the
@@ -1569,8 +1631,9 @@ __global__ void __launch_bounds__(LB_TPB) k_msg_scatter(uint32_t n, const uint32
 #define LB_MSM_W 4
 #define LB_MSM_B (1 << LB_MSM_C)
 #define LB_MSM_NB (LB_MSM_W * LB_MSM_B)  // bucket ids w * 256 + d (d = 0 unused)
+// (set_live == nullptr: every decoded set; the caller masks the terms later, k_g2_sum_g8)
 __device__ __forceinline__ bool msm_live(uint32_t i, const uint32_t* set_live, const uint32_t* sig_inf) {
-  return set_live[i] && !sig_inf[i];
+  return (set_live == nullptr || set_live[i]) && !sig_inf[i];
 }
 #if LB_KG(6)
 __global__ void __launch_bounds__(LB_TPB) k_msm_count(uint32_t n, const uint64_t* __restrict__ scalars,
@@ -1998,11 +2061,13 @@ __global__ void __launch_bounds__(LBR_NT) k_sig_blind_row(uint32_t n, const uint
 #if LB_KG(9)
 __global__ void __launch_bounds__(8 * LB_SUM_G8_GROUPS) k_g2_sum_g8(uint32_t n, const uint32_t* __restrict__ in,
                                                                   uint32_t n_out, uint32_t* __restrict__ out,
-                                                                  uint32_t out0) {
+                                                                  uint32_t out0, const uint32_t* __restrict__ live) {
+  // live (optional): term i counts iff live[i] (terms computed before the job statuses were known)
   __shared__ uint32_t st[LB_SUM_G8_GROUPS * 72];
   const int g = threadIdx.x >> 3, q = g8_q();
   g2j acc = jac_infinity<fp2>();
-  for (uint32_t i = g; i < n; i += LB_SUM_G8_GROUPS) g8_add(acc, soa_ld<g2j>(in, n, i));
+  for (uint32_t i = g; i < n; i += LB_SUM_G8_GROUPS)
+    if (live == nullptr || live[i]) g8_add(acc, soa_ld<g2j>(in, n, i));
   auto stash = [&](int slot, const g2j& v) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
     LB_UNROLL for (int k = 0; k < 9; k++) st[slot * 72 + 8 * k + q] = w[8 * k + q];
