@@ -574,7 +574,7 @@ int32_t lb_engine_create_ex(int32_t device, uint32_t flags, lb_engine** out) {
                              nullptr, nullptr, nullptr);
           hipLaunchKernelGGL(k_pk_chunks, dim3(4096), dim3(LB_TPB), 0, e->stream3, 0u, nullptr, nullptr, nullptr, nullptr);
           // the row r PK ladder (one row per set), at the largest small batch
-          hipLaunchKernelGGL(k_pk_blind_rowp, dim3(std::max<uint32_t>(1u, (e->row_max + 3) / 4)), dim3(64), 0, e->stream3,
+          hipLaunchKernelGGL(k_pk_blind_rowp, dim3(std::max<uint32_t>(1u, e->row_max)), dim3(64), 0, e->stream3,
                              0u, nullptr, nullptr, nullptr, nullptr);
         }
         if (res23 >= 2) {
@@ -700,14 +700,17 @@ static int32_t batch_fill(lb_engine* e, lb_batch* b, uint32_t n_jobs, const uint
     if (r != hipSuccess || !bytes) return r;
     return hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, e->stream);
   };
-  // chunk decomposition of every set's pubkey range (<= LB_PK_CHUNK keys per chunk)
+  // chunk decomposition of every set's pubkey range (<= LB_PK_CHUNK keys per chunk; a small batch,
+  // whose aggregation is latency -- a block's 131 sets of ~256 keys --, <= LB_PK_CHUNK_SMALL: its
+  // serial chain per lane 16 -> 4 mixed additions before the six-level segmented tree)
   std::vector<uint32_t>& set_chunk_off = b->h_set_chunk_off;
   std::vector<uint32_t>& chunk_lo = b->h_chunk_lo;
   set_chunk_off.resize(n_sets + 1);
   chunk_lo.clear();
+  const uint32_t pkc = n_sets <= e->row_max ? LB_PK_CHUNK_SMALL : LB_PK_CHUNK;
   for (uint32_t i = 0; i < n_sets; i++) {
     set_chunk_off[i] = (uint32_t)chunk_lo.size();
-    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += LB_PK_CHUNK)
+    for (uint32_t k = set_pk_offsets[i]; k < set_pk_offsets[i + 1]; k += pkc)
       chunk_lo.push_back(k | (k == set_pk_offsets[i] ? LB_CHUNK_FIRST : 0u));  // flag: the set's first chunk
   }
   set_chunk_off[n_sets] = (uint32_t)chunk_lo.size();
@@ -1133,7 +1136,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       if (e->straus_run) LB_HIP(e->pk3.ensure((size_t)ns * sizeof(g1x3)));
       for (uint32_t mode = m0; mode <= m1; mode++) {
         if (mode == 2u && pk_rowp) {
-          hipLaunchKernelGGL(k_pk_blind_rowp, dim3((n + 3) / 4), dim3(64), 0, s3, n, e->pk_aff.as<uint32_t>(),
+          hipLaunchKernelGGL(k_pk_blind_rowp, dim3(n), dim3(64), 0, s3, n, e->pk_aff.as<uint32_t>(),
                              e->scalars.as<uint64_t>(), e->rpk.as<uint32_t>(), e->pk_status.as<int32_t>());
           continue;
         }

@@ -902,6 +902,9 @@ __global__ void __launch_bounds__(LBR_NT) k_hash_finish_row(uint32_t n, const ui
 // keys so a 512-key sync aggregate costs one chunk's latency plus a short combine instead of
 // 512 serial additions on one lane; chunk c covers pubkeys [chunk_lo[c], chunk_lo[c+1]) of one set.
 #define LB_PK_CHUNK 16
+#ifndef LB_PK_CHUNK_SMALL
+#define LB_PK_CHUNK_SMALL 4  // ... for batches of up to row_max sets (lb_engine.hip batch_fill)
+#endif
 // chunk_lo[c] bit 31: chunk c is its set's first (lb_engine.hip batch_fill; the sentinel
 // chunk_lo[nc] carries it too)
 #define LB_CHUNK_FIRST 0x80000000u
@@ -1155,22 +1158,24 @@ __global__ void __launch_bounds__(LB_INV_TPB, LB_MINW_G1) k_pk_blind(uint32_t n,
 }
 #endif  // LB_KG
 
-// k_pk_blind's mode 2 (the r PK ladder, from mode 1's pk_status / pk_aff) with one 16-lane row per
-// set, 4 sets per wave, every product a row product (lb_row.h rfp: the same generic GLV ladder,
-// jac_mul_glv_i<rfp>), for small batches on a device running alone: a C2 block's ladders are
-// ~600 serial lone-lane products each (~0.9 ms), here row products (~0.45 us each).
+// k_pk_blind's mode 2 (the r PK ladder, from mode 1's pk_status / pk_aff) for small batches on a
+// device running alone: ONE WAVE per set, its four rows four product units (lb_row.h w4_mul: every
+// row holds the whole state, each level's independent products one per row, the results handed to
+// every row by permlane swaps).  A doubling (dbl-2009-l) is 3 product levels, a doubling plus a
+// mixed addition (madd-2007-bl) 6 (the addition's first products ride along with the doubling's),
+// against 7 and 18 serial products: a C2 block's ladders ~0.9 ms of lone-lane products (round 5),
+// ~0.45 ms with one row per set, ~0.1 ms here.
 #if LB_KG(13)
 __global__ void __launch_bounds__(64) k_pk_blind_rowp(uint32_t n, const uint32_t* __restrict__ pk_aff,
                                                      const uint64_t* __restrict__ scalars, uint32_t* __restrict__ rpk,
                                                      const int32_t* __restrict__ pk_status) {
-  if (n == 0) return;  // (the scratch reservation's empty dispatch)
-  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 4;
-  const uint32_t ic = i < n ? i : n - 1;  // rows past the end redo the last set
-  const int st = pk_status[ic];
-  const uint64_t w = scalars[ic];
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;  // (n = 0: the scratch reservation's empty dispatch)
+  const int st = pk_status[i];
+  const uint64_t w = scalars[i];
   g1j rj = jac_infinity<fp>();
-  if (st == LB_OK) {
-    const g1a pk = soa_ld<g1a>(pk_aff, n, ic);
+  if (st == LB_OK) {  // uniform (one set per wave)
+    const g1a pk = soa_ld<g1a>(pk_aff, n, i);
     if (w == 1) {  // the unblinded 1-set call: r PK = PK, affine (Z = 1)
       rj = g1j{pk.x, pk.y, fp_one()};
     } else {
@@ -1189,30 +1194,49 @@ __global__ void __launch_bounds__(64) k_pk_blind_rowp(uint32_t n, const uint32_t
       int b = 31;
       while (b > 0 && digit(b) == 0) b--;  // w != 0 (the engine's scalars are non-zero)
       auto tab = [&](uint32_t d) { return d == 1u ? t1 : (d == 2u ? t2 : t3); };
-      jac<rfp> acc = jac_from_aff(tab(digit(b)));
+      const aff<rfp> top = tab(digit(b));
+      rfp X = top.x, Y = top.y, Z;
+      f_set_one(Z);
       for (b--; b >= 0; b--) {
-        acc = jac_dbl_i(acc);
-        const uint32_t d = digit(b);
-        if (d != 0u) {  // madd-2007-bl without the tests
-          const aff<rfp> q = tab(d);
-          const rfp Z1Z1 = f_sqr(acc.z);
-          const rfp H = f_sub(f_mul(q.x, Z1Z1), acc.x);
-          const rfp rr = f_dbl(f_sub(f_mul(f_mul(q.y, acc.z), Z1Z1), acc.y));
-          const rfp HH = f_sqr(H);
-          const rfp I = f_dbl(f_dbl(HH));
-          const rfp J = f_mul(H, I);
-          const rfp V = f_mul(acc.x, I);
-          jac<rfp> r;
-          r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-          r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(acc.y, J)));
-          r.z = f_sub(f_sub(f_sqr(f_add(acc.z, H)), Z1Z1), HH);
-          acc = r;
+        const uint32_t d = digit(b);  // uniform
+        // doubling: A = X^2, B = Y^2, YZ; C = B^2, P = (X + B)^2, F = E^2 (E = 3A); E (D - X3)
+        rfp o[4];
+        w4_mul<3>({X, Y, Y}, {X, Y, Z}, o);
+        const rfp A = o[0], B = o[1], Z3 = f_dbl(o[2]), E = f_mul3(A), XB = f_add(X, B);
+        if (d == 0u) {
+          w4_mul<3>({B, XB, E}, {B, XB, E}, o);
+          const rfp C = o[0], D = f_dbl(f_sub(f_sub(o[1], A), C));
+          X = f_sub(o[2], f_dbl(D));
+          w4_mul<1>({E}, {f_sub(D, X)}, o);
+          Y = f_sub(o[0], f_mul8(C));
+          Z = Z3;
+          continue;
         }
+        const aff<rfp> q = tab(d);
+        // ... with the addition's Z1Z1 = Z3^2 alongside
+        w4_mul<4>({B, XB, E, Z3}, {B, XB, E, Z3}, o);
+        const rfp C = o[0], D = f_dbl(f_sub(f_sub(o[1], A), C)), Z1Z1 = o[3];
+        const rfp X3 = f_sub(o[2], f_dbl(D));
+        // E (D - X3); U2 = x2 Z1Z1; y2 Z3
+        w4_mul<3>({E, q.x, q.y}, {f_sub(D, X3), Z1Z1, Z3}, o);
+        const rfp Y3 = f_sub(o[0], f_mul8(C)), H = f_sub(o[1], X3), Y2Z = o[2];
+        // S2 = y2 Z3 Z1Z1; HH = H^2; (Z3 + H)^2
+        const rfp ZH = f_add(Z3, H);
+        w4_mul<3>({Y2Z, H, ZH}, {Z1Z1, H, ZH}, o);
+        const rfp rr = f_dbl(f_sub(o[0], Y3)), HH = o[1], I = f_dbl(f_dbl(HH));
+        Z = f_sub(f_sub(o[2], Z1Z1), HH);
+        // J = H I; V = X3 I; rr^2
+        w4_mul<3>({H, X3, rr}, {I, I, rr}, o);
+        const rfp J = o[0], V = o[1];
+        X = f_sub(f_sub(o[2], J), f_dbl(V));
+        // rr (V - X); Y3 J
+        w4_mul<2>({rr, Y3}, {f_sub(V, X), J}, o);
+        Y = f_sub(o[0], f_dbl(o[1]));
       }
-      rj = rf_fp(acc);
+      rj = rf_fp(jac<rfp>{X, Y, Z});
     }
   }
-  if (i < n && (threadIdx.x & 15) == 0) aos_st(rpk, i, rj);
+  if (threadIdx.x == 0) aos_st(rpk, i, rj);
 }
 #endif  // LB_KG
 

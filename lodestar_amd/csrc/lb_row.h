@@ -836,6 +836,36 @@ __device__ __forceinline__ void f_set_one(rfp& a) { a = rf_of(fp_one()); }
 __device__ __forceinline__ aff<rfp> rf_of(const g1a& a) { return aff<rfp>{rf_of(a.x), rf_of(a.y)}; }
 __device__ __forceinline__ g1j rf_fp(const jac<rfp>& a) { return g1j{rf_fp(a.x), rf_fp(a.y), rf_fp(a.z)}; }
 
+// ---- the four rows of a wave as four product units for ONE item (every row holds the whole
+// state, the same values): w4_mul computes up to four independent products in one row product,
+// row j the j-th, and hands every row all four results (three v_permlane*_swap, VALU ops).
+// permlane16_swap(v, v) = {rows (v0 v0 v2 v2), rows (v1 v1 v3 v3)}; permlane32_swap(u, u) of those:
+// {(u0 u0 u0 u0) -> v0 / v1, (u2 ...) -> v2 / v3}.
+__device__ __forceinline__ void w4_gather(int v, int (&o)[4]) {
+  const auto e = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const auto a = __builtin_amdgcn_permlane32_swap(e[0], e[0], false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(e[1], e[1], false, false);
+  o[0] = a[0];
+  o[1] = b[0];
+  o[2] = a[1];
+  o[3] = b[1];
+}
+template <int N>
+__device__ __forceinline__ void w4_mul(const rfp (&x)[N], const rfp (&y)[N], rfp* o) {
+  static_assert(N >= 1 && N <= 4, "w4_mul: one product per row");
+  const int r = (threadIdx.x >> 4) & 3;
+  int xv = x[0].v, yv = y[0].v;
+  LB_UNROLL for (int j = 1; j < N; j++) {
+    xv = r == j ? x[j].v : xv;
+    yv = r == j ? y[j].v : yv;
+  }
+  int xr[14];
+  r_rep(xv, xr);
+  int g[4];
+  w4_gather(rp_mul(xr, yv, r_limb()), g);
+  LB_UNROLL for (int j = 0; j < N; j++) o[j].v = g[j];
+}
+
 // rfp2: Fp2 over rfp (Karatsuba products: three row products), and the map_to_curve_g2_fold_t
 // policy (lb_h2c.h: fl_*)
 struct rfp2 {
