@@ -1162,7 +1162,10 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
       if (sb_par) LB_HIP(hipEventRecord(e->ev_sdec, s2));
       // (8 lanes per signature also for a slot while the device is otherwise idle ran slower:
       // 13.5 vs 13.0 ms per slot, profiles/r3_idle_forms_ab.txt)
-      if (n <= e->row_max && e->alone && e->row_fe)
+      if (n <= e->row_max && e->alone && e->row_fe && e->small_par)  // one wave per signature (round 6)
+        hipLaunchKernelGGL(k_sig_subgroup_w4, dim3(n), dim3(64), 0, s2, n, e->sig_aff.as<uint32_t>(),
+                           e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>());
+      else if (n <= e->row_max && e->alone && e->row_fe)
         hipLaunchKernelGGL(k_sig_subgroup_row, dim3(n), dim3(LBR_NT), 0, s2, n, e->sig_aff.as<uint32_t>(),
                            e->sig_inf.as<uint32_t>(), e->sig_status.as<int32_t>(), e->row_proj ? 1u : 0u);
       else if (n <= e->subgroup_g8_max)
@@ -1186,9 +1189,8 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
         e->used[ST_SIG_MSM] = true;
       }
       LB_HIP(e->s_terms.ensure((size_t)n * sizeof(g2j)));
-      hipLaunchKernelGGL(k_sig_blind_row, dim3(n), dim3(LBR_NT), 0, s3, n, e->sig_aff.as<uint32_t>(),
-                         e->scalars.as<uint64_t>(), nullptr, e->sig_inf.as<uint32_t>(), e->s_terms.as<uint32_t>(),
-                         e->row_proj ? 1u : 0u);
+      hipLaunchKernelGGL(k_sig_blind_w4, dim3(n), dim3(64), 0, s3, n, e->sig_aff.as<uint32_t>(),
+                         e->scalars.as<uint64_t>(), e->sig_inf.as<uint32_t>(), e->s_terms.as<uint32_t>());
       LB_HIP(hipEventRecord(e->ev_sblind, s3));
     }
     // ---- s1: group the sets by signing root

@@ -1197,46 +1197,127 @@ __global__ void __launch_bounds__(64) k_pk_blind_rowp(uint32_t n, const uint32_t
       const aff<rfp> top = tab(digit(b));
       rfp X = top.x, Y = top.y, Z;
       f_set_one(Z);
+      // lazy sums inside a step (lb_row.h lz_*: |v| < 32 p as product operands), the carried point
+      // reduced at its end
       for (b--; b >= 0; b--) {
         const uint32_t d = digit(b);  // uniform
         // doubling: A = X^2, B = Y^2, YZ; C = B^2, P = (X + B)^2, F = E^2 (E = 3A); E (D - X3)
         rfp o[4];
         w4_mul<3>({X, Y, Y}, {X, Y, Z}, o);
-        const rfp A = o[0], B = o[1], Z3 = f_dbl(o[2]), E = f_mul3(A), XB = f_add(X, B);
+        const rfp A = o[0], B = o[1], E = lz_mul(A, 3), XB = lz_add(X, B);
+        const rfp Z3 = rf_red(2 * (int64_t)o[2].v);
         if (d == 0u) {
           w4_mul<3>({B, XB, E}, {B, XB, E}, o);
-          const rfp C = o[0], D = f_dbl(f_sub(f_sub(o[1], A), C));
-          X = f_sub(o[2], f_dbl(D));
-          w4_mul<1>({E}, {f_sub(D, X)}, o);
-          Y = f_sub(o[0], f_mul8(C));
+          const rfp C = o[0], D = lz_mul(lz_sub(lz_sub(o[1], A), C), 2);
+          X = rf_red((int64_t)o[2].v - 2 * (int64_t)D.v);
+          w4_mul<1>({E}, {lz_sub(D, X)}, o);
+          Y = rf_red((int64_t)o[0].v - 8 * (int64_t)C.v);
           Z = Z3;
           continue;
         }
         const aff<rfp> q = tab(d);
         // ... with the addition's Z1Z1 = Z3^2 alongside
         w4_mul<4>({B, XB, E, Z3}, {B, XB, E, Z3}, o);
-        const rfp C = o[0], D = f_dbl(f_sub(f_sub(o[1], A), C)), Z1Z1 = o[3];
-        const rfp X3 = f_sub(o[2], f_dbl(D));
+        const rfp C = o[0], D = lz_mul(lz_sub(lz_sub(o[1], A), C), 2), Z1Z1 = o[3];
+        const rfp X3 = rf_red((int64_t)o[2].v - 2 * (int64_t)D.v);
         // E (D - X3); U2 = x2 Z1Z1; y2 Z3
-        w4_mul<3>({E, q.x, q.y}, {f_sub(D, X3), Z1Z1, Z3}, o);
-        const rfp Y3 = f_sub(o[0], f_mul8(C)), H = f_sub(o[1], X3), Y2Z = o[2];
+        w4_mul<3>({E, q.x, q.y}, {lz_sub(D, X3), Z1Z1, Z3}, o);
+        const rfp Y3 = rf_red((int64_t)o[0].v - 8 * (int64_t)C.v), H = lz_sub(o[1], X3), Y2Z = o[2];
         // S2 = y2 Z3 Z1Z1; HH = H^2; (Z3 + H)^2
-        const rfp ZH = f_add(Z3, H);
+        const rfp ZH = lz_add(Z3, H);
         w4_mul<3>({Y2Z, H, ZH}, {Z1Z1, H, ZH}, o);
-        const rfp rr = f_dbl(f_sub(o[0], Y3)), HH = o[1], I = f_dbl(f_dbl(HH));
-        Z = f_sub(f_sub(o[2], Z1Z1), HH);
+        const rfp rr = lz_mul(lz_sub(o[0], Y3), 2), HH = o[1], I = lz_mul(HH, 4);
+        Z = rf_red((int64_t)o[2].v - Z1Z1.v - HH.v);
         // J = H I; V = X3 I; rr^2
         w4_mul<3>({H, X3, rr}, {I, I, rr}, o);
         const rfp J = o[0], V = o[1];
-        X = f_sub(f_sub(o[2], J), f_dbl(V));
+        X = rf_red((int64_t)o[2].v - J.v - 2 * (int64_t)V.v);
         // rr (V - X); Y3 J
-        w4_mul<2>({rr, Y3}, {f_sub(V, X), J}, o);
-        Y = f_sub(o[0], f_dbl(o[1]));
+        w4_mul<2>({rr, Y3}, {lz_sub(V, X), J}, o);
+        Y = rf_red((int64_t)o[0].v - 2 * (int64_t)o[1].v);
       }
       rj = rf_fp(jac<rfp>{X, Y, Z});
     }
   }
   if (threadIdx.x == 0) aos_st(rpk, i, rj);
+}
+#endif  // LB_KG
+
+// Small batches on a device running alone, one WAVE per signature (lb_row.h w4_g2_*: the four
+// rows of the wave as four product units; a doubling in 4 product levels, a mixed addition in 8):
+// the 16-wave row-engine kernels need a whole CU each, and a block's 131 subgroup checks, 131
+// r_i sig_i ladders and ~70 cofactor clearings (k_hash_finish_row) asked for more CUs than the
+// device has, so the per-root chain waited for CUs.
+// The subgroup check: Scott's psi(P) == [x]P as k_sig_subgroup, [|x|]P without the exceptional
+// additions; a zero final Z (an exceptional case on the way, the inputs being adversarial, or
+// [|x|]P = O) reruns the lane ladder with the tested additions (g2_aff_in_subgroup_i).
+#if LB_KG(13)
+__global__ void __launch_bounds__(64) k_sig_subgroup_w4(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                       const uint32_t* __restrict__ sig_inf,
+                                                       int32_t* __restrict__ sig_status) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  if (sig_status[i] != LB_OK || sig_inf[i]) return;  // uniform
+  const g2a P = soa_ld<g2a>(sig_aff, n, i);
+  const rfp2* t2 = nullptr;
+  const rfp2 px = fl_in(P.x, t2), py = fl_in(P.y, t2);
+  rfp2 X = px, Y = py, Z;
+  f_set_one(Z);
+#pragma clang loop unroll(disable)
+  for (int b = 62; b >= 0; b--) {
+    w4_g2_dbl(X, Y, Z);
+    if ((LB_X_ABS >> b) & 1ull) w4_g2_madd(X, Y, Z, px, py);
+  }
+  bool ok;
+  if (fp2_is_zero(fl_out(Z))) {
+    ok = g2_aff_in_subgroup_i(P);
+  } else {
+    // psi(P) = (conj(x) cx, conj(y) cy) == -[|x|]P = (X / Z^2, -Y / Z^3)
+    const rfp2 Z2 = f_sqr(Z);
+    const rfp2 sx = f_mul(fl_conj(px), fl_in(fp2_load(LB_PSI_CX), t2));
+    const rfp2 sy = f_mul(fl_conj(py), fl_in(fp2_load(LB_PSI_CY), t2));
+    ok = fp2_eq(fl_out(f_mul(sx, Z2)), fl_out(X)) && fp2_eq(fl_out(f_mul(f_mul(sy, Z2), Z)), fl_out(f_neg(Y)));
+  }
+  if (!ok && threadIdx.x == 0) sig_status[i] = LB_POINT_NOT_IN_GROUP;
+}
+#endif  // LB_KG
+// r_i sig_i of every decoded set (k_sig_blind_row's GLV double-and-add over sig, [lambda] sig =
+// -psi^2(sig), [1 + lambda] sig = -psi^4(sig), all affine) without the exceptional additions: for
+// sig in G2 the running scalar never meets +-T_d (the GLV lattice argument of k_pk_blind_rowp);
+// a set whose signature is not in G2 is not live, and k_g2_sum_g8 masks its term.
+#if LB_KG(13)
+__global__ void __launch_bounds__(64) k_sig_blind_w4(uint32_t n, const uint32_t* __restrict__ sig_aff,
+                                                    const uint64_t* __restrict__ scalars,
+                                                    const uint32_t* __restrict__ sig_inf, uint32_t* __restrict__ terms) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;  // (n = 0: the scratch reservation's empty dispatch)
+  const uint64_t w = scalars[i];
+  g2j r = jac_infinity<fp2>();
+  if (!sig_inf[i] && w != 0) {  // uniform
+    const g2a S = soa_ld<g2a>(sig_aff, n, i);
+    const rfp2* t2p = nullptr;
+    const rfp* t1p = nullptr;
+    const rfp2 x1 = fl_in(S.x, t2p), y1 = fl_in(S.y, t2p);
+    const rfp c2x = fl_in(fp_load(LB_PSI2_CX), t1p), c2y = fl_in(fp_load(LB_PSI2_CY), t1p);
+    const rfp c4x = fl_in(fp_load(LB_PSI4_CX), t1p), c4y = fl_in(fp_load(LB_PSI4_CY), t1p);
+    const rfp2 x2 = fl_mulb(x1, c2x), y2 = f_neg(fl_mulb(y1, c2y));
+    const rfp2 x3 = fl_mulb(x1, c4x), y3 = f_neg(fl_mulb(y1, c4y));
+    const uint32_t k0 = (uint32_t)w, k1 = (uint32_t)(w >> 32);
+    auto digit = [&](int b) { return ((k0 >> b) & 1u) | (((k1 >> b) & 1u) << 1); };
+    int b = 31;
+    while (b > 0 && digit(b) == 0) b--;
+    const uint32_t d0 = digit(b);
+    rfp2 X = d0 == 1u ? x1 : (d0 == 2u ? x2 : x3), Y = d0 == 1u ? y1 : (d0 == 2u ? y2 : y3), Z;
+    f_set_one(Z);
+#pragma clang loop unroll(disable)
+    for (b--; b >= 0; b--) {
+      w4_g2_dbl(X, Y, Z);
+      const uint32_t d = digit(b);  // uniform
+      if (d != 0u) w4_g2_madd(X, Y, Z, d == 1u ? x1 : (d == 2u ? x2 : x3), d == 1u ? y1 : (d == 2u ? y2 : y3));
+    }
+    r = g2j{fl_out(X), fl_out(Y), fl_out(Z)};
+  }
+  if (threadIdx.x == 0) soa_st(terms, n, i, r);
 }
 #endif  // LB_KG
 

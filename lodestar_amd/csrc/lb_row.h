@@ -904,12 +904,110 @@ __device__ __forceinline__ rfp fl_norm(const rfp2& a) { return f_add(f_sqr(a.c0)
 __device__ __forceinline__ rfp2 fl_mulb(const rfp2& a, const rfp& s) { return rfp2{f_mul(a.c0, s), f_mul(a.c1, s)}; }
 __device__ __forceinline__ rfp2 fl_conj(const rfp2& a) { return rfp2{a.c0, f_neg(a.c1)}; }
 __device__ __forceinline__ rfp2 fl_make(const rfp& a, const rfp& b) { return rfp2{a, b}; }
+__device__ __forceinline__ rfp2 f_mul3(const rfp2& a) { return rfp2{f_mul3(a.c0), f_mul3(a.c1)}; }
+__device__ __forceinline__ rfp2 f_mul8(const rfp2& a) { return rfp2{f_mul8(a.c0), f_mul8(a.c1)}; }
 __device__ __forceinline__ rfp fl_c0(const rfp2& a) { return a.c0; }
 __device__ __forceinline__ rfp fl_c1(const rfp2& a) { return a.c1; }
 __device__ __forceinline__ void f_set_zero(rfp2& a) { a.c0.v = a.c1.v = 0; }
 __device__ __forceinline__ void f_set_one(rfp2& a) {
   f_set_one(a.c0);
   a.c1.v = 0;
+}
+
+// ---- G2 in Jacobian coordinates over rfp2 on the four rows of a wave (w4_mul levels of four Fp
+// products; every row holds the point): one wave per point instead of a 16-wave row-engine
+// workgroup, for the small-batch ladders (k_sig_subgroup_w4, k_sig_blind_w4).  No exceptional-case
+// tests: any exceptional case of the formulas (an operand at infinity, P = +-Q, Y = 0) yields Z = 0,
+// which every later doubling and mixed addition keeps (as the row engine's fast chains).
+__device__ __forceinline__ rfp rf_lz(int64_t v) { return rfp{r_norm<true>(v, r_limb())}; }  // carries only
+__device__ __forceinline__ rfp rf_sum(const rfp& a, const rfp& b) { return rf_lz((int64_t)a.v + b.v); }
+__device__ __forceinline__ rfp rf_dif(const rfp& a, const rfp& b) { return rf_lz((int64_t)a.v - b.v); }
+// lazy sums (carry rounds only, no quotient-estimate reduction): a value stays a valid product
+// operand while its coefficients sum to <= 16 over reduced / product-output terms (|v| < 32 p);
+// the ladders reduce only the point they carry from step to step (f_* below)
+__device__ __forceinline__ rfp lz_add(const rfp& a, const rfp& b) { return rf_lz((int64_t)a.v + b.v); }
+__device__ __forceinline__ rfp lz_sub(const rfp& a, const rfp& b) { return rf_lz((int64_t)a.v - b.v); }
+__device__ __forceinline__ rfp lz_mul(const rfp& a, int c) { return rf_lz((int64_t)c * a.v); }
+__device__ __forceinline__ rfp2 lz_add(const rfp2& a, const rfp2& b) { return rfp2{lz_add(a.c0, b.c0), lz_add(a.c1, b.c1)}; }
+__device__ __forceinline__ rfp2 lz_sub(const rfp2& a, const rfp2& b) { return rfp2{lz_sub(a.c0, b.c0), lz_sub(a.c1, b.c1)}; }
+__device__ __forceinline__ rfp2 lz_mul(const rfp2& a, int c) { return rfp2{lz_mul(a.c0, c), lz_mul(a.c1, c)}; }
+// Karatsuba's third product t2 = (a0 + a1)(b0 + b1) -> (t0 - t1, t2 - t0 - t1), lazy (< 2p, 3p)
+__device__ __forceinline__ rfp2 rf2_kara(const rfp& t0, const rfp& t1, const rfp& t2) {
+  return rfp2{lz_sub(t0, t1), rf_lz((int64_t)t2.v - t0.v - t1.v)};
+}
+// the complex squaring's (o0, 2 o1)
+__device__ __forceinline__ rfp2 rf2_sq(const rfp& o0, const rfp& o1) { return rfp2{o0, lz_mul(o1, 2)}; }
+// reduce the limb-wise combination sum_j c_j a_j (64-bit limb sums) of each component
+#define RF2_RED(E0, E1) (rfp2{rf_red((int64_t)(E0)), rf_red((int64_t)(E1))})
+#define I64(x) ((int64_t)(x))
+// dbl-2009-l: A = X^2, B = Y^2 | C = B^2, F = E^2 (E = 3A) | P = (X + B)^2, y0 z0, y1 z1 |
+// (y0 + y1)(z0 + z1), E (D - X3): four levels of four products.  In: X, Y, Z reduced (< p); out
+// reduced.  Bounds (in p): A, B, C, F, P < 2; E < 6; D < 12; X3 reduced; W < 13.
+__device__ __forceinline__ void w4_g2_dbl(rfp2& X, rfp2& Y, rfp2& Z) {
+  rfp o[4];
+  w4_mul<4>({rf_sum(X.c0, X.c1), X.c0, rf_sum(Y.c0, Y.c1), Y.c0}, {rf_dif(X.c0, X.c1), X.c1, rf_dif(Y.c0, Y.c1), Y.c1}, o);
+  const rfp2 A = rf2_sq(o[0], o[1]), B = rf2_sq(o[2], o[3]);
+  const rfp2 E = lz_mul(A, 3);
+  w4_mul<4>({rf_sum(B.c0, B.c1), B.c0, rf_sum(E.c0, E.c1), E.c0}, {rf_dif(B.c0, B.c1), B.c1, rf_dif(E.c0, E.c1), E.c1}, o);
+  const rfp2 C = rf2_sq(o[0], o[1]), F = rf2_sq(o[2], o[3]);
+  const rfp2 XB = lz_add(X, B);
+  w4_mul<4>({rf_sum(XB.c0, XB.c1), XB.c0, Y.c0, Y.c1}, {rf_dif(XB.c0, XB.c1), XB.c1, Z.c0, Z.c1}, o);
+  const rfp2 P = rf2_sq(o[0], o[1]);
+  const rfp yz0 = o[2], yz1 = o[3];
+  const rfp2 D = lz_mul(lz_sub(lz_sub(P, A), C), 2);
+  const rfp2 X3 = RF2_RED(I64(F.c0.v) - 2 * I64(D.c0.v), I64(F.c1.v) - 2 * I64(D.c1.v));
+  const rfp2 W = lz_sub(D, X3);
+  w4_mul<4>({rf_sum(Y.c0, Y.c1), E.c0, E.c1, rf_sum(E.c0, E.c1)}, {rf_sum(Z.c0, Z.c1), W.c0, W.c1, rf_sum(W.c0, W.c1)}, o);
+  const rfp2 YZ = rf2_kara(yz0, yz1, o[0]);
+  const rfp2 EW = rf2_kara(o[1], o[2], o[3]);
+  Y = RF2_RED(I64(EW.c0.v) - 8 * I64(C.c0.v), I64(EW.c1.v) - 8 * I64(C.c1.v));
+  X = X3;
+  Z = RF2_RED(2 * I64(YZ.c0.v), 2 * I64(YZ.c1.v));
+}
+// madd-2007-bl (Q affine, reduced): 29 products in eight levels.  In / out as w4_g2_dbl.
+// Bounds (in p): Z1Z1, HH < 2; U2, S2, J, V < 3; H < 4; ZH < 5; R < 8; I < 8; W < 4.
+__device__ __forceinline__ void w4_g2_madd(rfp2& X, rfp2& Y, rfp2& Z, const rfp2& qx, const rfp2& qy) {
+  rfp o[4];
+  // Z1Z1 = Z1^2; qy0 z0, qy1 z1
+  w4_mul<4>({rf_sum(Z.c0, Z.c1), Z.c0, qy.c0, qy.c1}, {rf_dif(Z.c0, Z.c1), Z.c1, Z.c0, Z.c1}, o);
+  const rfp2 ZZ = rf2_sq(o[0], o[1]);
+  const rfp a0 = o[2], a1 = o[3];
+  // (qy0 + qy1)(z0 + z1); U2 = qx Z1Z1
+  w4_mul<4>({rf_sum(qy.c0, qy.c1), qx.c0, qx.c1, rf_sum(qx.c0, qx.c1)}, {rf_sum(Z.c0, Z.c1), ZZ.c0, ZZ.c1, rf_sum(ZZ.c0, ZZ.c1)}, o);
+  const rfp2 QZ = rf2_kara(a0, a1, o[0]);
+  const rfp2 U2 = rf2_kara(o[1], o[2], o[3]);
+  const rfp2 H = lz_sub(U2, X);
+  // S2 = qy Z1 Z1Z1; (h0 + h1)(h0 - h1)
+  w4_mul<4>({QZ.c0, QZ.c1, rf_sum(QZ.c0, QZ.c1), rf_sum(H.c0, H.c1)}, {ZZ.c0, ZZ.c1, rf_sum(ZZ.c0, ZZ.c1), rf_dif(H.c0, H.c1)}, o);
+  const rfp2 S2 = rf2_kara(o[0], o[1], o[2]);
+  const rfp hh0 = o[3];
+  const rfp2 R = lz_mul(lz_sub(S2, Y), 2);
+  const rfp2 ZH = lz_add(Z, H);
+  // h0 h1; (Z1 + H)^2; (r0 + r1)(r0 - r1)
+  w4_mul<4>({H.c0, rf_sum(ZH.c0, ZH.c1), ZH.c0, rf_sum(R.c0, R.c1)}, {H.c1, rf_dif(ZH.c0, ZH.c1), ZH.c1, rf_dif(R.c0, R.c1)}, o);
+  const rfp2 HH = rf2_sq(hh0, o[0]), ZH2 = rf2_sq(o[1], o[2]);
+  const rfp r2a = o[3];
+  const rfp2 I = lz_mul(HH, 4);
+  // r0 r1; J = H I
+  w4_mul<4>({R.c0, H.c0, H.c1, rf_sum(H.c0, H.c1)}, {R.c1, I.c0, I.c1, rf_sum(I.c0, I.c1)}, o);
+  const rfp2 R2 = rf2_sq(r2a, o[0]);
+  const rfp2 J = rf2_kara(o[1], o[2], o[3]);
+  // V = X1 I; y0 j0
+  w4_mul<4>({X.c0, X.c1, rf_sum(X.c0, X.c1), Y.c0}, {I.c0, I.c1, rf_sum(I.c0, I.c1), J.c0}, o);
+  const rfp2 V = rf2_kara(o[0], o[1], o[2]);
+  const rfp yj0 = o[3];
+  const rfp2 X3 = RF2_RED(I64(R2.c0.v) - I64(J.c0.v) - 2 * I64(V.c0.v), I64(R2.c1.v) - I64(J.c1.v) - 2 * I64(V.c1.v));
+  const rfp2 W = lz_sub(V, X3);
+  // r W; y1 j1
+  w4_mul<4>({R.c0, R.c1, rf_sum(R.c0, R.c1), Y.c1}, {W.c0, W.c1, rf_sum(W.c0, W.c1), J.c1}, o);
+  const rfp2 RW = rf2_kara(o[0], o[1], o[2]);
+  const rfp yj1 = o[3];
+  // (y0 + y1)(j0 + j1)
+  w4_mul<1>({rf_sum(Y.c0, Y.c1)}, {rf_sum(J.c0, J.c1)}, o);
+  const rfp2 YJ = rf2_kara(yj0, yj1, o[0]);
+  Y = RF2_RED(I64(RW.c0.v) - 2 * I64(YJ.c0.v), I64(RW.c1.v) - 2 * I64(YJ.c1.v));
+  X = X3;
+  Z = RF2_RED(I64(ZH2.c0.v) - I64(ZZ.c0.v) - I64(HH.c0.v), I64(ZH2.c1.v) - I64(ZZ.c1.v) - I64(HH.c1.v));
 }
 
 // An Fp exponentiation by a constant on a PAIR of rows (rows 2j, 2j + 1 of a wave; every lane of

@@ -43,7 +43,7 @@ GROUPS = {
     10: ["k_miller_row", "k_tree_up_row"],
     11: ["k_ml_S_row", "k_root_check_row", "k_root_partial_row", "k_partials_check_row"],
     12: ["k_hash_finish_row", "k_sig_blind_row", "k_sig_subgroup_row"],
-    13: ["k_hash_map_row", "k_decompress_sigs_row", "k_pk_blind_rowp"],
+    13: ["k_hash_map_row", "k_decompress_sigs_row", "k_pk_blind_rowp", "k_sig_subgroup_w4", "k_sig_blind_w4"],
 }
 N_GROUPS = len(GROUPS)
 GROUP_OF = {k: g for g, ks in GROUPS.items() for k in ks}
