@@ -27,6 +27,7 @@
 #pragma once
 #include "lb_pairing.h"
 #include "lb_row_progs.h"
+#include "lb_pdbl_tab.h"
 
 #ifndef LBR_WAVES
 #define LBR_WAVES 16  // one workgroup of 16 waves (4 per SIMD): a phase of <= 64 products in one round
@@ -684,8 +685,113 @@ __device__ void r_sqr(int32_t* S, int dst, int a) {
   r_exec(S, LBR_SQR12);
   r_out(S, LBR_SQR12, 0, 12, dst);
 }
+// Granger-Scott cyclotomic squaring written out for the workgroup instead of interpreted
+// (CSQR12): the interpreter's per-phase work -- program header and record reads, the next phase's
+// prefetch, the operand records, the IN / output copies of r_run -- cost ~2.2 us of a 3.1 us
+// squaring (profiles/r6_row_bench_tl.txt), the 18 products ~0.9 us.  Here each row's task follows
+// from its row number:
+//   products (rows 0..17): pair q = row / 6 of (x, y) in {(a00, a11), (a10, a02), (a01, a12)},
+//     j = row % 6: x^2 = ((x0 + x1)(x0 - x1), 2 x0 x1), y^2 likewise, (x + y)^2 likewise;
+//   outputs (rows 0..11), Fp4 squares r0 = xi y^2 + x^2, r1 = (x + y)^2 - x^2 - y^2:
+//     c00 = 3 t0.r0 - 2 a00, c01 = 3 t1.r0 - 2 a01, c02 = 3 t2.r0 - 2 a02,
+//     c10 = 3 xi t2.r1 + 2 a10, c11 = 3 t0.r1 + 2 a11, c12 = 3 t1.r1 + 2 a12
+// (tools/gen_row_programs.py cyclotomic_sqr; slot k = c{k/6}.c{(k%6)/2}.c{k%2}).  Two barriers per
+// squaring; dst may equal src (output k reads only input k).
+#ifndef LBR_CSQR_FAST
+#define LBR_CSQR_FAST 1
+#endif
+__device__ __forceinline__ void r_csqr_fast(int32_t* S_generic, int dst, int src) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row();
+  const int T = LBR_TEMP;
+  if (row < 18) {
+    const int q = row / 6, j = row - 6 * q;
+    const int xs = q == 0 ? 0 : (q == 1 ? 6 : 2), ys = q == 0 ? 8 : (q == 1 ? 4 : 10);
+    const int x0 = S[16 * (src + xs) + k], x1 = S[16 * (src + xs + 1) + k];
+    const int y0 = S[16 * (src + ys) + k], y1 = S[16 * (src + ys + 1) + k];
+    // coefficients of (x0, x1, y0, y1) in the product's two operands, by j
+    const int ax0 = (j == 0 || j == 1 || j >= 4) ? 1 : 0, ax1 = (j == 0 || j == 4) ? 1 : 0;
+    const int ay0 = (j == 2 || j == 3 || j >= 4) ? 1 : 0, ay1 = (j == 2 || j == 4) ? 1 : 0;
+    const int bx0 = (j == 0 || j == 4) ? 1 : 0, bx1 = (j == 0 || j == 4) ? -1 : (j == 1 || j == 5 ? 1 : 0);
+    const int by0 = (j == 2 || j == 4) ? 1 : 0, by1 = (j == 2 || j == 4) ? -1 : (j == 3 || j == 5 ? 1 : 0);
+    const int xv = r_norm<true>((int64_t)ax0 * x0 + (int64_t)ax1 * x1 + (int64_t)ay0 * y0 + (int64_t)ay1 * y1, k);
+    const int yv = r_norm<true>((int64_t)bx0 * x0 + (int64_t)bx1 * x1 + (int64_t)by0 * y0 + (int64_t)by1 * y1, k);
+    int xr[14];
+    r_rep(xv, xr);
+    S[16 * (T + row) + k] = rp_mul(xr, yv, k);
+  }
+  r_sync();
+  if (row < 12) {
+    // output row -> pair q and form: 0 r0.c0, 1 r0.c1, 2 r1.c0, 3 r1.c1, 4 (xi r1).c0, 5 (xi r1).c1
+    const int q = (row < 2 || row == 8 || row == 9) ? 0 : ((row < 4 || row >= 10) ? 1 : 2);
+    const int f = row < 6 ? (row & 1) : (row < 8 ? 4 + (row & 1) : 2 + (row & 1));
+    // coefficients of the pair's products p0..p5 and of the input slot, per form
+    const int c0 = f == 0 ? 3 : ((f == 1 || f == 3) ? 0 : -3);
+    const int c1 = f == 1 ? 6 : (f == 3 ? -6 : (f == 4 ? 6 : (f == 5 ? -6 : 0)));
+    const int c2 = f < 2 ? 3 : (f == 3 ? 0 : -3);
+    const int c3 = f == 0 ? -6 : (f == 1 ? 6 : (f == 2 ? 0 : (f == 4 ? 6 : -6)));
+    const int c4 = f >= 2 && f != 3 ? 3 : 0;
+    const int c5 = f == 3 ? 6 : (f == 4 ? -6 : (f == 5 ? 6 : 0));
+    const int ci = f < 2 ? -2 : 2;
+    const int b = T + 6 * q;
+    int64_t acc = (int64_t)ci * S[16 * (src + row) + k];
+    acc += (int64_t)c0 * S[16 * (b + 0) + k] + (int64_t)c1 * S[16 * (b + 1) + k] + (int64_t)c2 * S[16 * (b + 2) + k];
+    acc += (int64_t)c3 * S[16 * (b + 3) + k] + (int64_t)c4 * S[16 * (b + 4) + k] + (int64_t)c5 * S[16 * (b + 5) + k];
+    S[16 * (dst + row) + k] = r_reduce(acc, k);
+  }
+  r_sync();
+}
+
+// The projective G2 doubling (RCB Algorithm 9, PDBL1) written out the same way: phase 1, rows
+// 0..9: the level-1 products P (Y^2, YZ, Z^2, XY); phase 2, rows 0..11: the four Fp2 products of
+// level 2 (Karatsuba) over combinations of P; phase 3, rows 0..5: the outputs.  Each row's integer
+// coefficients come from tools/gen_pdbl_fast.py (lb_pdbl_tab.h), which checks the three phases
+// against the oracle's doubling.  dst may equal src.
+#ifndef LBR_PDBL_FAST
+#define LBR_PDBL_FAST 1
+#endif
+__device__ __forceinline__ void r_pdbl_fast(int32_t* S_generic, int dst, int src) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row();
+  const int T = LBR_TEMP;  // P at T .. T + 9, Q at T + 10 .. T + 21
+  if (row < 10) {
+    int64_t x = 0, y = 0;
+    LB_UNROLL for (int e = 0; e < 6; e++) {
+      const int v = S[16 * (src + e) + k];
+      x += (int64_t)LBR_PD1[row][e] * v;
+      y += (int64_t)LBR_PD1[row][6 + e] * v;
+    }
+    int xr[14];
+    r_rep(r_norm<true>(x, k), xr);
+    S[16 * (T + row) + k] = rp_mul(xr, r_norm<true>(y, k), k);
+  }
+  r_sync();
+  if (row < 12) {
+    int64_t x = 0, y = 0;
+    LB_UNROLL for (int e = 0; e < 10; e++) {
+      const int v = S[16 * (T + e) + k];
+      x += (int64_t)LBR_PD2[row][e] * v;
+      y += (int64_t)LBR_PD2[row][10 + e] * v;
+    }
+    int xr[14];
+    r_rep(r_reduce(x, k), xr);
+    S[16 * (T + 10 + row) + k] = rp_mul(xr, r_reduce(y, k), k);
+  }
+  r_sync();
+  if (row < 6) {
+    int64_t acc = 0;
+    LB_UNROLL for (int e = 0; e < 12; e++) acc += (int64_t)LBR_PD3[row][e] * S[16 * (T + 10 + e) + k];
+    S[16 * (dst + row) + k] = r_reduce(acc, k);
+  }
+  r_sync();
+}
+
 // a^2 for a in the cyclotomic subgroup (Granger-Scott: 18 products instead of 36)
 __device__ void r_csqr(int32_t* S, int dst, int a) {
+  if (LBR_CSQR_FAST) {
+    r_csqr_fast(S, dst, a);
+    return;
+  }
   r_copy(S, LBR_IN, a, 12);
   r_exec(S, LBR_CSQR12);
   r_out(S, LBR_CSQR12, 0, 12, dst);
@@ -1264,6 +1370,17 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
     }
     if (kind == RK_COPY) {
       r_copy(S_generic, dst, a, b);
+      continue;
+    }
+    if (LBR_PDBL_FAST && (kind == RK_PDBL || kind == RK_PDBL2 || kind == RK_PDBL4)) {
+      const int nd = kind == RK_PDBL ? 1 : (kind == RK_PDBL2 ? 2 : 4);
+      r_pdbl_fast(S_generic, dst, a);
+      for (int q = 1; q < nd; q++) r_pdbl_fast(S_generic, dst, dst);
+      continue;
+    }
+    if (LBR_CSQR_FAST && (kind == RK_CSQR || kind == RK_CSQR2)) {
+      r_csqr_fast(S_generic, dst, a);
+      if (kind == RK_CSQR2) r_csqr_fast(S_generic, dst, dst);
       continue;
     }
     if (kind == RK_G2NEG) {  // in place (dst == a)
