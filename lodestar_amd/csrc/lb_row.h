@@ -28,6 +28,7 @@
 #include "lb_pairing.h"
 #include "lb_row_progs.h"
 #include "lb_pdbl_tab.h"
+#include "lb_mul12_tab.h"
 
 #ifndef LBR_WAVES
 #define LBR_WAVES 16  // one workgroup of 16 waves (4 per SIMD): a phase of <= 64 products in one round
@@ -675,7 +676,43 @@ __device__ void r_init(int32_t* S_generic, int nprog = LBR_PROGS_FE, int first =
 }
 
 // ---------------------------------------------------------------- Fp12 ops on 12-slot areas
+// The Fp12 product (MUL12) written out the same way: phase 1, rows 0..53: the 54 Karatsuba
+// products, each operand a sum of <= 8 input slots (a: 0..11, b: 12..23); phase 2, rows 0..11: the
+// outputs, <= 36 product terms each (tools/gen_mul12_fast.py -> lb_mul12_tab.h, checked against
+// the oracle's tower product).  dst may equal a or b.
+#ifndef LBR_MUL12_FAST
+#define LBR_MUL12_FAST 1
+#endif
+__device__ __forceinline__ void r_mul12_fast(int32_t* S_generic, int dst, int a, int b) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row();
+  const int T = LBR_TEMP;
+  if (row < 54) {
+    int64_t x = 0, y = 0;
+    LB_UNROLL for (int j = 0; j < LBR_M12_NX; j++) {
+      const int sx = LBR_M12P[row][2 * j], sy = LBR_M12P[row][2 * LBR_M12_NX + 2 * j];
+      x += (int64_t)LBR_M12P[row][2 * j + 1] * S[16 * (sx < 12 ? a + sx : b + sx - 12) + k];
+      y += (int64_t)LBR_M12P[row][2 * LBR_M12_NX + 2 * j + 1] * S[16 * (sy < 12 ? a + sy : b + sy - 12) + k];
+    }
+    int xr[14];
+    r_rep(r_norm<true>(x, k), xr);
+    S[16 * (T + row) + k] = rp_mul(xr, r_norm<true>(y, k), k);
+  }
+  r_sync();
+  if (row < 12) {
+    int64_t acc = 0;
+    LB_UNROLL for (int j = 0; j < LBR_M12_NO; j++)
+      acc += (int64_t)LBR_M12O[row][2 * j + 1] * S[16 * (T + LBR_M12O[row][2 * j]) + k];
+    S[16 * (dst + row) + k] = r_reduce(acc, k);
+  }
+  r_sync();
+}
+
 __device__ void r_mul(int32_t* S, int dst, int a, int b) {
+  if (LBR_MUL12_FAST) {
+    r_mul12_fast(S, dst, a, b);
+    return;
+  }
   r_gather(S, LBR_IN, 24, [&](int e) { return e < 12 ? a + e : b + e - 12; });
   r_exec(S, LBR_MUL12);
   r_out(S, LBR_MUL12, 0, 12, dst);
@@ -1376,6 +1413,10 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
       const int nd = kind == RK_PDBL ? 1 : (kind == RK_PDBL2 ? 2 : 4);
       r_pdbl_fast(S_generic, dst, a);
       for (int q = 1; q < nd; q++) r_pdbl_fast(S_generic, dst, dst);
+      continue;
+    }
+    if (LBR_MUL12_FAST && kind == RK_MUL) {
+      r_mul12_fast(S_generic, dst, a, b);
       continue;
     }
     if (LBR_CSQR_FAST && (kind == RK_CSQR || kind == RK_CSQR2)) {

@@ -117,3 +117,34 @@ def test_written_out_pdbl_and_csqr_on_the_row_model():
         s = csqr(s)
         want = o.f12_sqr(want)
     assert [R.from_row(l) for l in s] == flat(want)
+
+
+def test_written_out_mul12_on_the_row_model():
+    """lb_row.h r_mul12_fast (tools/gen_mul12_fast.py tables: 54 Karatsuba products, carry-only
+    operand sums, reduced outputs) on the row engine's exact arithmetic, chained, against the
+    oracle's Fp12 product; the committed lb_mul12_tab.h equal to a fresh render."""
+    import gen_row_programs as R
+    import gen_mul12_fast as M
+    from oracle import bls_oracle as o
+    assert M.check()
+    with open(os.path.join(ROOT, "lodestar_amd", "csrc", "lb_mul12_tab.h")) as f:
+        assert f.read() == M.emit(), "lb_mul12_tab.h is stale: python tools/gen_mul12_fast.py"
+    prods, flat = M.tables()
+
+    def mul(sa, sb):
+        vin = sa + sb
+        pv = [R.rp_mul(R.lin([(c, vin[k]) for k, c in x.items()], reduce=False),
+                       R.lin([(c, vin[k]) for k, c in y.items()], reduce=False)) for x, y in prods]
+        return [R.lin([(c, pv[k]) for k, c in f.items()]) for f in flat]
+
+    rnd = random.Random(12)
+    tw = lambda v: tuple(tuple((v[6 * h + 2 * j], v[6 * h + 2 * j + 1]) for j in range(3)) for h in range(2))
+    flatf = lambda a: [c for h in a for x in h for c in x]
+    a = [rnd.randrange(o.P) for _ in range(12)]
+    acc, want = [R.to_row(v) for v in a], tw(a)
+    for _ in range(5):
+        b = [rnd.randrange(o.P) for _ in range(12)]
+        acc = mul(acc, [R.to_row(v) for v in b])
+        want = o.f12_mul(want, tw(b))
+        assert all(-2 <= x < (1 << 28) + 3 for l in acc for x in l[:13])
+    assert [R.from_row(l) for l in acc] == flatf(want)
