@@ -29,6 +29,7 @@
 #include "lb_row_progs.h"
 #include "lb_pdbl_tab.h"
 #include "lb_mul12_tab.h"
+#include "lb_row_compiled.h"
 
 #ifndef LBR_WAVES
 #define LBR_WAVES 16  // one workgroup of 16 waves (4 per SIMD): a phase of <= 64 products in one round
@@ -1393,6 +1394,97 @@ static __device__ const r_opl LBR_OPS_XLADDER = r_ops_xladder(LBR_A(4), LBR_A(3)
 static_assert(r_ops_fe_tail(LBR_A(0), LBR_A(0)).n <= LBR_MAX_OPS && r_ops_hash_finish(LBR_A(4), LBR_A(3)).n <= LBR_MAX_OPS,
               "lb_row.h: op list size");
 
+// ---------------------------------------------------------------- compiled programs
+// The Miller loop's step programs (DBL_STEP, ADD_STEP) run by a fixed-phase executor instead of
+// the interpreter: each phase's kind, flags and term counts are compile-time constants
+// (tools/gen_row_compiled.py -> lb_row_compiled.h), so a phase is straight-line code; a row reads
+// its own record (dst, operand pairs) from a per-row table; the program's input slots (IN) are
+// mapped to the operation's sources instead of copied in (one copy phase and barrier fewer).
+#ifndef LBR_ML_COMPILED
+#define LBR_ML_COMPILED 1
+#endif
+struct rc_dbl_step {
+  static constexpr int NPH = LBC_DBL_STEP_NPH, RS = LBC_DBL_STEP_RS, NOUT = LBC_DBL_STEP_NOUT;
+  static constexpr int ph(int p, int f) { return LBC_DBL_STEP_PH[p][f]; }
+  __device__ static const int32_t* rec(int p, int row) { return &LBC_DBL_STEP_REC[p][row][0]; }
+  __device__ static int out(int e) { return LBC_DBL_STEP_OUT[e]; }
+};
+struct rc_add_step {
+  static constexpr int NPH = LBC_ADD_STEP_NPH, RS = LBC_ADD_STEP_RS, NOUT = LBC_ADD_STEP_NOUT;
+  static constexpr int ph(int p, int f) { return LBC_ADD_STEP_PH[p][f]; }
+  __device__ static const int32_t* rec(int p, int row) { return &LBC_ADD_STEP_REC[p][row][0]; }
+  __device__ static int out(int e) { return LBC_ADD_STEP_OUT[e]; }
+};
+template <int N, class M>
+__device__ __forceinline__ int64_t rc_acc(const lds_i32* S, const int* w, int k, M map) {
+  int64_t acc = 0;
+  LB_UNROLL for (int j = 0; j < N; j++) acc += (int64_t)(w[j] >> 16) * S[16 * map(w[j] & 0xffff) + k];
+  return acc;
+}
+template <class P, int I>
+struct rc_w {
+  static constexpr int n = 1 + P::ph(I, 3) + P::ph(I, 4);  // record words of phase I
+};
+template <class P, int I>
+__device__ __forceinline__ void rc_load(int row, int (&w)[rc_w<P, I>::n]) {
+  const int32_t* rec = P::rec(I, row);
+  LB_UNROLL for (int j = 0; j < rc_w<P, I>::n; j++) w[j] = rec[j];
+}
+// phase I with its record already in registers; phase I + 1's record is loaded before this
+// phase's operand reads (software pipelining: the table read overlaps the phase's work)
+template <class P, int I, class M>
+__device__ __forceinline__ void rc_phases(lds_i32* S, int k, int row, int pk, M map, const int (&w)[rc_w<P, I>::n]) {
+  constexpr int kind = P::ph(I, 0), flags = P::ph(I, 1), nx = P::ph(I, 3), ny = P::ph(I, 4), bar = P::ph(I, 5);
+  constexpr int IN = I + 1 < P::NPH ? I + 1 : I;
+  int wn[rc_w<P, IN>::n];
+  if constexpr (I + 1 < P::NPH) rc_load<P, IN>(row, wn);
+  const int dst = w[0];
+  if (dst >= 0) {  // uniform within the row
+    if constexpr (kind == 0) {
+      int xv, yv;
+      if constexpr ((flags & 1) != 0) xv = S[16 * map(w[1] & 0xffff) + k];
+      else {
+        const int64_t a = rc_acc<nx>(S, w + 1, k, map);
+        xv = (flags & 4) ? r_reduce(a, k, pk) : r_norm<true>(a, k);
+      }
+      if constexpr ((flags & 2) != 0) yv = S[16 * map(w[1 + nx] & 0xffff) + k];
+      else {
+        const int64_t a = rc_acc<ny>(S, w + 1 + nx, k, map);
+        yv = (flags & 8) ? r_reduce(a, k, pk) : r_norm<true>(a, k);
+      }
+      int xr[14];
+      r_rep(xv, xr);
+      S[16 * dst + k] = rp_mul(xr, yv, k);
+    } else {
+      S[16 * dst + k] = r_reduce(rc_acc<nx>(S, w + 1, k, map), k, pk);
+    }
+  }
+  if constexpr (bar != 0) r_sync();
+  if constexpr (I + 1 < P::NPH) rc_phases<P, I + 1>(S, k, row, pk, map, wn);
+}
+// a Miller step on the areas of r_run: f at `f` (12 slots), T at tt (6), P at pp (2), Q at qq (4,
+// ADD_STEP); outputs f <- f^2 l (or f l), T <- 2T (or T + Q)
+template <class P>
+__device__ __forceinline__ void rc_miller_step(int32_t* S_generic, int f, int tt, int pp, int qq, bool add) {
+  lds_i32* S = r_lds(S_generic);
+  const int k = r_limb(), row = r_row(), pk = r_plimb(k);
+  auto map = [&](int s) -> int {
+    if (s >= 24) return s;  // (LBR_IN = 0: the program's inputs are slots 0 .. 23)
+    if (s < 12) return f + s;
+    if (s < 18) return tt + s - 12;
+    if (!add) return pp + s - 18;
+    return s < 22 ? qq + s - 18 : pp + s - 22;
+  };
+  int w0[rc_w<P, 0>::n];
+  rc_load<P, 0>(row, w0);
+  rc_phases<P, 0>(S, k, row, pk, map, w0);
+  for (int e = row; e < P::NOUT; e += LBR_NROWS) {
+    const int d = e < 12 ? f + e : tt + e - 12;
+    S[16 * d + k] = S[16 * P::out(e) + k];
+  }
+  r_sync();
+}
+
 // run ops[0, n): every program through one inlined interpreter
 __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl* ops, int n) {
   lds_i32* S = r_lds(S_generic);
@@ -1472,6 +1564,18 @@ __device__ __attribute__((noinline)) void r_run(int32_t* S_generic, const r_opl*
       S[16 * d + k] = S[16 * pr[2 + e] + k];
     }
     r_sync();
+  }
+}
+
+// the Miller loop's op list (only RK_MLDBL / RK_MLADD) on the compiled steps; a separate function
+// so the other op lists' interpreter (r_run) keeps its code size
+__device__ __attribute__((noinline)) void r_run_ml(int32_t* S_generic, const r_opl* ops, int n) {
+  const int PP = LBR_PT, QQ = LBR_PT + 2, TT = LBR_PT + 6;
+  for (int i = 0; i < n; i++) {
+    const int w0 = __builtin_amdgcn_readfirstlane(ops->w[2 * i]);
+    const int kind = w0 & 0xffff, dst = w0 >> 16;
+    if (kind == RK_MLDBL) rc_miller_step<rc_dbl_step>(S_generic, dst, TT, PP, QQ, false);
+    else rc_miller_step<rc_add_step>(S_generic, dst, TT, PP, QQ, true);
   }
 }
 
@@ -1561,7 +1665,8 @@ __device__ void r_miller(int32_t* S_generic, int dst) {
   }
 #ifndef LBR_NO_OPLIST
   if (dst == LBR_A(0) || dst == LBR_A(7)) {
-    r_run(S_generic, dst == LBR_A(0) ? &LBR_OPS_ML_A0 : &LBR_OPS_ML_A7, LBR_OPS_ML_A0.n);
+    if (LBR_ML_COMPILED) r_run_ml(S_generic, dst == LBR_A(0) ? &LBR_OPS_ML_A0 : &LBR_OPS_ML_A7, LBR_OPS_ML_A0.n);
+    else r_run(S_generic, dst == LBR_A(0) ? &LBR_OPS_ML_A0 : &LBR_OPS_ML_A7, LBR_OPS_ML_A0.n);
     r_conj(S_generic, dst, dst);
     return;
   }

@@ -148,3 +148,13 @@ def test_written_out_mul12_on_the_row_model():
         want = o.f12_mul(want, tw(b))
         assert all(-2 <= x < (1 << 28) + 3 for l in acc for x in l[:13])
     assert [R.from_row(l) for l in acc] == flatf(want)
+
+
+def test_compiled_miller_steps_on_the_row_model():
+    """lb_row.h rc_miller_step's compiled DBL_STEP / ADD_STEP (tools/gen_row_compiled.py: the
+    interpreter's phases decoded into per-row records, one task per row) replayed on the row
+    arithmetic against the interpreter's own replay; lb_row_compiled.h equal to a fresh render."""
+    import gen_row_compiled as C
+    assert C.check()
+    with open(os.path.join(ROOT, "lodestar_amd", "csrc", "lb_row_compiled.h")) as f:
+        assert f.read() == C.emit(), "lb_row_compiled.h is stale: python tools/gen_row_compiled.py"
