@@ -17,6 +17,10 @@
 #ifndef LB_H2C_FOLD
 #define LB_H2C_FOLD 1
 #endif
+// rfp2 products on the four rows of a wave (lb_row.h f_mul / f_sqr; k_hash_map_row one item per wave)
+#ifndef LBR_FP2_W4
+#define LBR_FP2_W4 1
+#endif
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>

@@ -1270,7 +1270,7 @@ static int32_t run_pipeline(lb_engine* e, lb_batch* b, const uint64_t* scalars, 
     {
       stage_scope sc(e, ST_HASH_MAP, s1);
       if (nuh <= e->hash_row_max && e->alone && e->row_fe)
-        hipLaunchKernelGGL(k_hash_map_row, dim3(LB_H2C_FOLD ? nuh : (2 * nuh + 3) / 4), dim3(64), 0, s1, n, nuh,
+        hipLaunchKernelGGL(k_hash_map_row, dim3(LB_H2C_FOLD ? (LBR_FP2_W4 ? 2 * nuh : nuh) : (2 * nuh + 3) / 4), dim3(64), 0, s1, n, nuh,
                            e->uniq_set.as<uint32_t>(), b->d_msgs.as<uint8_t>(), e->q.as<uint32_t>());
       else
         hipLaunchKernelGGL(k_hash_map, dim3(nblk(2 * nuh)), dim3(LB_TPB), 0, s1, n, nuh, e->uniq_set.as<uint32_t>(),

@@ -609,8 +609,13 @@ __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, co
 #if LB_H2C_FOLD
   // two items per wave, a row PAIR each: map_to_curve_g2_fold with row products (rfp2 / rfp) and
   // the exponentiations on the pair (r2_pow_rf)
+#if LBR_FP2_W4
+  const uint32_t t = blockIdx.x;  // one item per wave (rfp2 products on its four rows)
+  if (t >= 2 * nu) return;        // (whole wave)
+#else
   const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 5;
   if (blockIdx.x * 2 >= 2 * nu) return;  // (whole wave)
+#endif
   const uint32_t tc = t < 2 * nu ? t : 2 * nu - 1;
   const uint32_t which = tc < nu ? 0u : 1u;
   const uint32_t u = which ? tc - nu : tc;
@@ -623,7 +628,7 @@ __global__ void __launch_bounds__(64) k_hash_map_row(uint32_t n, uint32_t nu, co
   }
   const g2j r = map_to_curve_g2_fold_t<rfp2, rfp>(hash_to_field_u(M, (int)which),
                                                 [](const rfp& a, const uint32_t* e, int top) { return r2_pow_rf(a, e, top); });
-  if (t < 2 * nu && (threadIdx.x & 31) == 0) soa_st(q, 2 * n, which * n + u, r);
+  if (t < 2 * nu && (threadIdx.x & (LBR_FP2_W4 ? 63 : 31)) == 0) soa_st(q, 2 * n, which * n + u, r);
 #else
   const uint32_t t = (blockIdx.x * 64 + threadIdx.x) >> 4;
   if (blockIdx.x * 4 >= 2 * nu) return;  // (whole wave)

@@ -1019,7 +1019,20 @@ __device__ __forceinline__ rfp2 f_add(const rfp2& a, const rfp2& b) { return rfp
 __device__ __forceinline__ rfp2 f_sub(const rfp2& a, const rfp2& b) { return rfp2{f_sub(a.c0, b.c0), f_sub(a.c1, b.c1)}; }
 __device__ __forceinline__ rfp2 f_neg(const rfp2& a) { return rfp2{f_neg(a.c0), f_neg(a.c1)}; }
 __device__ __forceinline__ rfp2 f_dbl(const rfp2& a) { return rfp2{f_dbl(a.c0), f_dbl(a.c1)}; }
+// LBR_FP2_W4 (default): every rfp2 user runs one item per WAVE (the four rows hold the same
+// values), so the Karatsuba products take one row product on rows 0..2 (w4_mul) instead of three
+// in sequence on each row
 __device__ __forceinline__ rfp2 f_mul(const rfp2& a, const rfp2& b) {
+#if LBR_FP2_W4
+  {
+    const int k = r_limb();
+    const rfp x[3] = {a.c0, a.c1, rfp{r_norm<true>((int64_t)a.c0.v + a.c1.v, k)}};
+    const rfp y[3] = {b.c0, b.c1, rfp{r_norm<true>((int64_t)b.c0.v + b.c1.v, k)}};
+    rfp t[3];
+    w4_mul<3>(x, y, t);
+    return rfp2{rf_red((int64_t)t[0].v - t[1].v), rf_red((int64_t)t[2].v - t[0].v - t[1].v)};
+  }
+#endif
   const rfp t0 = f_mul(a.c0, b.c0), t1 = f_mul(a.c1, b.c1);
   const int k = r_limb();
   // (a0 + a1)(b0 + b1): operand sums by carry rounds only (|sum| < 4p, a valid rp_mul operand)
@@ -1030,6 +1043,15 @@ __device__ __forceinline__ rfp2 f_mul(const rfp2& a, const rfp2& b) {
 }
 __device__ __forceinline__ rfp2 f_sqr(const rfp2& a) {
   const int k = r_limb();
+#if LBR_FP2_W4
+  {
+    const rfp x[2] = {rfp{r_norm<true>((int64_t)a.c0.v + a.c1.v, k)}, a.c0};
+    const rfp y[2] = {rfp{r_norm<true>((int64_t)a.c0.v - a.c1.v, k)}, a.c1};
+    rfp t[2];
+    w4_mul<2>(x, y, t);
+    return rfp2{t[0], f_dbl(t[1])};
+  }
+#endif
   int x[14];
   r_rep(r_norm<true>((int64_t)a.c0.v + a.c1.v, k), x);
   const int t0 = rp_mul(x, r_norm<true>((int64_t)a.c0.v - a.c1.v, k), k);
